@@ -1,0 +1,189 @@
+#!/usr/bin/env python3
+"""Benchmark: vectorized LoadBalancerK8sEnv env-steps/s on MI355X (BASELINE.json config 3).
+
+One bench "step" = one vector step of every env on every GPU: a uniform-random policy
+kernel (lb_policy RANDOM, action_space.sample() semantics) writes the actions, then the
+fused step kernel (lb_step: take_action + reward + next_request + get_state + auto-reset)
+consumes them.  Observations, rewards and dones go into a T-deep device ring, the shape
+of PPO's rollout storage (ppo_deepset.py:136-143), so writes stream to HBM instead of
+sitting in the 256 MB Infinity Cache.  Inputs (env state) are resident in HBM.
+
+Default workload: 2^20 default-scenario envs per GPU (E=8, N=24, Z=4, rejection, naive,
+episode_length 100; Philox seed 0).  Multi-GPU: one process per GPU, env ids sharded
+[rank*B, (rank+1)*B) with no data-path collective ("scaling": "weak").
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "gym-loadbalancing_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "env-steps/sec (whole node) at 1M envs, 1/2/4/8 GPUs; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+CONFIGS = {
+    "default": dict(),  # constructor defaults, loadbalancer_k8s_env.py:42-54
+    "cfg1": dict(num_endpoints=6, num_nodes=48, num_zones=12, reward_function="naive",
+                 latency_weight=1.0, cpu_weight=0.0, gini_weight=0.0),
+    "e64_multi": dict(num_endpoints=64, reward_function="multi", latency_weight=1.0,
+                      cpu_weight=0.0, gini_weight=0.0),
+}
+
+
+def algorithmic_bytes(cfg):
+    """B_alg = 53*E + 6*Z + 240 (rejection) / + 208 (no rejection).
+
+    Z here is the observable zone block (zone ids are drawn in [0,4) whatever num_zones
+    is, loadbalancer_k8s_env.py:354), i.e. the survey's Z=4 default.
+    """
+    E = cfg.num_endpoints
+    Z = min(cfg.num_zones, 4) if cfg.num_zones >= 4 else cfg.num_zones
+    return 53 * E + 6 * Z + (240 if cfg.rejection_allowed else 208)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--envs-per-gpu", type=int, default=1 << 20)
+    ap.add_argument("--config", default="default", choices=sorted(CONFIGS))
+    ap.add_argument("--ring", type=int, default=16, help="rollout ring depth (obs slots)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg_kwargs, seconds):
+    """The C oracle (Philox mode, OpenMP over envs) on a bounded sample of the same workload."""
+    import numpy as np
+
+    from oracle import oracle
+    B = 1 << 16
+    orc = oracle.OracleBatch(cfg_kwargs, B, trace=False, seed=0)
+    orc.init()
+    orc.reset()
+    for _ in range(3):
+        orc.step(orc.policy_random())
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        a = orc.policy_random()
+        orc.step(a)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    _ = np.zeros(1)
+    return dict(value=B * steps / el, unit="env-steps/s", cores=oracle.num_threads(), kind="port",
+                sample=f"C oracle (oracle/lbk8s_oracle.c, OpenMP), {B} envs x {steps} vector steps "
+                       f"({el:.1f} s), same scenario, Philox seed 0, random policy")
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from lbk8s import LBVecEnv
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    B = args.envs_per_gpu
+    cfg_kwargs = CONFIGS[args.config]
+    env = LBVecEnv(B, device=dev, seed=0, env_id_offset=rank * B, as_tensors=True, **cfg_kwargs)
+    R = env.cfg.obs_rows
+    T = max(1, args.ring)
+    obs_ring = torch.empty((T, B, R, 8), dtype=torch.float32, device=dev)
+    rew_ring = torch.empty((T, B), dtype=torch.float32, device=dev)
+    done_ring = torch.empty((T, B), dtype=torch.uint8, device=dev)
+    actions = torch.empty(B, dtype=torch.int32, device=dev)
+    env.reset()
+
+    def one_step(i, ev=None):
+        env.policy("random", out=actions)
+        if ev is not None:
+            ev[0].record()
+        env.step_device(actions, obs_out=obs_ring[i % T], reward_out=rew_ring[i % T],
+                        done_out=done_ring[i % T])
+        if ev is not None:
+            ev[1].record()
+
+    for i in range(args.warmup):
+        one_step(i)
+    K = args.steps
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    # pass 1: wall clock of exactly K steps, barrier + synchronize on both sides
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(K):
+        one_step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    # pass 2: per-launch duration of the dominant kernel (lb_step) with events on its stream
+    torch.cuda.synchronize()
+    for i in range(K):
+        one_step(args.warmup + K + i, evs[i])
+    torch.cuda.synchronize()
+    step_ms = sum(a.elapsed_time(b) for a, b in evs) / K
+    assert env.status() == 0, "kernel flagged bad actions / unreset envs"
+
+    value = world * B * K / el
+    b_alg = algorithmic_bytes(env.cfg)
+    achieved = b_alg * B / (step_ms * 1e-3) / 1e9
+    traffic = None
+    try:
+        with open(args.pmc_json) as f:
+            pmc = json.load(f)
+        if pmc.get("config") == args.config and pmc.get("envs") == B:
+            traffic = pmc.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    line = {
+        "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": K,
+        "warmup": args.warmup, "ms_per_step": el / K * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (Philox seed 0 scenarios, uniform-random policy on device)",
+        "config": {"workload": f"config 3: {B} {args.config}-scenario envs per GPU "
+                               f"(E={env.cfg.num_endpoints}, N={env.cfg.num_nodes}, "
+                               f"Z={env.cfg.num_zones}, {env.cfg.reward_function}), obs ring T={T}",
+                   "envs_per_gpu": B, "total_envs": world * B, "scenario": args.config,
+                   "episode_length": env.cfg.episode_length, "parallelism": f"env-sharded x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "k_step (lb_step)", "kernel_ms": step_ms, "bytes_per_env_step": b_alg},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(cfg_kwargs, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,99 @@
+"""ctypes binding of liblbk8s.so (include/lbk8s.h).
+
+The library is built in-tree (gym-loadbalancing_amd/csrc/Makefile) next to this file.
+torch is imported BEFORE the library is loaded so that liblbk8s.so's dependency on
+libamdhip64.so.7 resolves (by soname) to the HIP runtime torch already loaded: one HIP
+runtime per process, so torch's streams and allocations are valid in our calls.
+There is no CPU fallback: if the library is missing, every entry point raises.
+"""
+import ctypes as C
+import os
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblbk8s.so")
+ABI_VERSION = 1
+
+LB_REWARD = {"naive": 0, "latency": 1, "fairness": 2, "multi": 3}
+LB_RNG_PHILOX, LB_RNG_TRACE = 0, 1
+LB_POLICY = {"topo": 0, "zone_cpu": 1, "endpoint_cpu": 2, "random": 3}
+LB_FIELD = {"endpoint_latency": 0, "endpoint_cpu_usage_percentage": 1,
+            "endpoint_topology_latency": 2, "endpoint_zone_cpu_capacity": 3, "endpoint_zone": 4,
+            "endpoint_node": 5, "avg_load_served": 6, "current_time": 7, "current_step": 8,
+            "request_zone": 9, "request_threshold": 10}
+PER_ENV_FIELDS = {"current_time", "current_step", "request_zone", "request_threshold"}
+LB_ST_K = 16
+LB_STATUS_BAD_ACTION, LB_STATUS_NOT_RESET = 1, 2
+
+
+class LBConfigC(C.Structure):
+    _fields_ = [("num_endpoints", C.c_int32), ("num_zones", C.c_int32), ("num_nodes", C.c_int32),
+                ("episode_length", C.c_int32), ("reward_fn", C.c_int32),
+                ("rejection_allowed", C.c_int32), ("auto_reset", C.c_int32), ("rng_mode", C.c_int32),
+                ("arrival_rate", C.c_double), ("call_duration", C.c_double),
+                ("latency_weight", C.c_double), ("cpu_weight", C.c_double),
+                ("gini_weight", C.c_double), ("seed", C.c_uint64), ("env_id_offset", C.c_int64)]
+
+
+TRACE_FIELDS = ["t0", "step_x1", "step_x2", "step_r", "step_n", "reset_lat0", "reset_topo",
+                "reset_ntype", "reset_nzone", "reset_ncpu", "reset_enode", "reset_x1", "reset_x2",
+                "reset_r", "reset_n"]
+
+
+class LBTraceC(C.Structure):
+    _fields_ = [(f, C.c_void_p) for f in TRACE_FIELDS]
+
+
+_lib = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def lib():
+    """Load liblbk8s.so (once). Raises NativeLibraryMissing if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  (share torch's HIP runtime, see module docstring)
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryMissing(
+            f"{LIB_PATH} not found: build it with `make -C gym-loadbalancing_amd/csrc` "
+            "(or __graft_entry__.build()); there is no CPU fallback")
+    L = C.CDLL(LIB_PATH)
+    vp, i64, i32 = C.c_void_p, C.c_int64, C.c_int32
+    cfgp = C.POINTER(LBConfigC)
+    trp = C.POINTER(LBTraceC)
+    L.lb_abi_version.restype = C.c_int
+    L.lb_last_error.restype = C.c_char_p
+    L.lb_validate_config.argtypes = [cfgp]
+    L.lb_state_bytes.argtypes = [cfgp, i64, C.POINTER(C.c_uint64)]
+    L.lb_init.argtypes = [vp, cfgp, i64, trp, vp]
+    L.lb_reset.argtypes = [vp, cfgp, i64, vp, vp, trp, vp]
+    L.lb_step.argtypes = [vp, cfgp, i64, vp, vp, vp, vp, vp, vp, trp, vp]
+    L.lb_policy.argtypes = [vp, cfgp, i64, i32, vp, vp]
+    L.lb_get_field.argtypes = [vp, cfgp, i64, i32, vp, vp]
+    L.lb_get_stats.argtypes = [vp, cfgp, i64, vp, vp]
+    L.lb_status.argtypes = [vp, cfgp, i64, vp, vp]
+    for f in ("lb_validate_config", "lb_state_bytes", "lb_init", "lb_reset", "lb_step", "lb_policy",
+              "lb_get_field", "lb_get_stats", "lb_status"):
+        getattr(L, f).restype = C.c_int
+    v = L.lb_abi_version()
+    if v != ABI_VERSION:
+        raise RuntimeError(f"liblbk8s.so ABI {v} != expected {ABI_VERSION}; rebuild it")
+    _lib = L
+    return L
+
+
+def check(rc):
+    """Raise on a non-zero return code, mirroring the reference's exception types."""
+    if rc == 0:
+        return
+    msg = lib().lb_last_error().decode()
+    if msg.startswith("IndexError"):
+        raise IndexError(msg)
+    raise RuntimeError(f"liblbk8s: {msg} (rc={rc})")
+
+
+EXPORTED_SYMBOLS = ("lb_abi_version", "lb_last_error", "lb_validate_config", "lb_state_bytes",
+                    "lb_init", "lb_reset", "lb_step", "lb_policy", "lb_get_field", "lb_get_stats",
+                    "lb_status")

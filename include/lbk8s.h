@@ -1,0 +1,171 @@
+/*
+ * lbk8s.h — C ABI of the MI355X-native vectorized LoadBalancerK8sEnv (liblbk8s.so).
+ *
+ * The drop-in boundary for the reference's env hot path: the Gym contract of
+ * /root/reference/envs/loadbalancer_k8s_env.py (reset() :290-400, step() :403-513,
+ * action_masks() :808-821) batched over B envs, as driven by SB3's SubprocVecEnv
+ * in run.py:95-127 / envs/ppo_deepset.py:145-189 / envs/dqn_deepset.py:116-156.
+ * The Python host side (gym-loadbalancing_amd/lbk8s) binds these with ctypes.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Every buffer (the opaque `state` blob, obs,
+ *    actions, traces) is device memory allocated and owned by the caller (PyTorch);
+ *    the library never allocates device memory.
+ *  - Every call is asynchronous on `stream` (a hipStream_t passed as void*; NULL =
+ *    the default stream).  No host synchronisation happens inside any call.
+ *  - Return 0 on success, <0 on error; lb_last_error() gives a thread-local message.
+ *  - The same (cfg, num_envs) must be passed to every call on one state blob.
+ *  - Limits: 1 <= E <= 256, num_nodes in [24, 256], num_zones >= 4 (the reference
+ *    hard-codes zone draws in [0,4) and endpoint hosts in [0,24) and raises
+ *    IndexError below those: :205,:242,:354,:380), 1 <= episode_length <= 1023.
+ */
+#ifndef LBK8S_H
+#define LBK8S_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LBK8S_ABI_VERSION 1
+
+/* reward_function names of loadbalancer_k8s_env.py:20-31 */
+enum { LB_REWARD_NAIVE = 0, LB_REWARD_LATENCY = 1, LB_REWARD_FAIRNESS = 2, LB_REWARD_MULTI = 3 };
+/* where random draws come from */
+enum { LB_RNG_PHILOX = 0, LB_RNG_TRACE = 1 };
+/* policies: the three greedy heuristics of envs/baselines.py:6-35, plus uniform random */
+enum {
+    LB_POLICY_TOPOLOGY_GREEDY = 0,     /* baselines.py:6-13  argmin endpoint_topology_latency   */
+    LB_POLICY_ZONE_CPU_GREEDY = 1,     /* baselines.py:16-24 argmax endpoint_zone_cpu_capacity   */
+    LB_POLICY_ENDPOINT_CPU_GREEDY = 2, /* baselines.py:27-35 argmin endpoint_cpu_usage_percentage */
+    LB_POLICY_RANDOM = 3               /* action_space.sample() equivalent, Philox-keyed         */
+};
+/* lb_get_field ids: the env attributes the reference exposes (baselines.py:13,24,35 read 2,3,1) */
+enum {
+    LB_FIELD_ENDPOINT_LATENCY = 0,          /* endpoint_latency            [B,E] */
+    LB_FIELD_ENDPOINT_CPU = 1,              /* endpoint_cpu_usage_percentage [B,E] */
+    LB_FIELD_ENDPOINT_TOPOLOGY_LATENCY = 2, /* endpoint_topology_latency   [B,E] */
+    LB_FIELD_ENDPOINT_ZONE_CPU_CAPACITY = 3,/* endpoint_zone_cpu_capacity  [B,E] */
+    LB_FIELD_ENDPOINT_ZONE = 4,             /* endpoint_zone               [B,E] */
+    LB_FIELD_ENDPOINT_NODE = 5,             /* endpoint_node               [B,E] */
+    LB_FIELD_LOAD_SERVED = 6,               /* avg_load_served             [B,E] */
+    LB_FIELD_CURRENT_TIME = 7,              /* current_time                [B]   */
+    LB_FIELD_CURRENT_STEP = 8,              /* current_step                [B]   */
+    LB_FIELD_REQUEST_ZONE = 9,              /* endpoint_request.input_zone [B]   */
+    LB_FIELD_REQUEST_THRESHOLD = 10,        /* endpoint_request.latency_threshold [B] */
+    LB_FIELD_DT = 11,                       /* dt of the current request   [B]   */
+    LB_FIELD_COUNT = 12
+};
+/* ep_stats row (double x LB_ST_K) written for every env whose episode ends in a step */
+enum {
+    LB_ST_RETURN = 0,       /* total_reward                                  */
+    LB_ST_LENGTH = 1,       /* current_step                                  */
+    LB_ST_ACCEPTED = 2,     /* ep_accepted_requests                          */
+    LB_ST_SUM_LATENCY = 3,  /* sum(avg_endpoint_latency list)                */
+    LB_ST_SUM_TOPOLOGY = 4, /* sum(avg_topology_latency list)                */
+    LB_ST_SUM_TOPOLOGY_UPDATED = 5, /* sum(avg_topology_latency_updated)     */
+    LB_ST_SUM_COST = 6,     /* sum(avg_cost list)                            */
+    LB_ST_SUM_CPU = 7,      /* sum(avg_cpu_usage_percentage_endpoint_selected) */
+    LB_ST_INTRA = 8,        /* intra_zone_requests                           */
+    LB_ST_INTER = 9,        /* inter_zone_requests                           */
+    LB_ST_GINI = 10,        /* calculate_gini_coefficient(avg_load_served)   */
+    LB_ST_EPISODE = 11,     /* episode index of this env (1-based)           */
+    LB_ST_K = 16
+};
+/* lb_status flag bits */
+enum { LB_STATUS_BAD_ACTION = 1, LB_STATUS_NOT_RESET = 2 };
+
+typedef struct lb_config {
+    int32_t num_endpoints;     /* E   (__init__ num_endpoints, :86)         */
+    int32_t num_zones;         /* Z                                           */
+    int32_t num_nodes;         /* N                                           */
+    int32_t episode_length;    /* done <=> current_step == episode_length (:472) */
+    int32_t reward_fn;         /* LB_REWARD_*                                 */
+    int32_t rejection_allowed; /* extra reject row + action E (:138-174)      */
+    int32_t auto_reset;        /* 1: VecEnv semantics, reset inside the done step */
+    int32_t rng_mode;          /* LB_RNG_*                                    */
+    double arrival_rate;       /* arrival_rate_r                              */
+    double call_duration;      /* call_duration_r                             */
+    double latency_weight, cpu_weight, gini_weight;
+    uint64_t seed;             /* Philox key                                  */
+    int64_t env_id_offset;     /* global id of this shard's env 0             */
+} lb_config;
+
+/*
+ * Injected draws (rng_mode == LB_RNG_TRACE): the values the reference's numpy
+ * Generator returned, per env, for ONE call.  Device pointers; unused ones may be NULL.
+ *   init : t0 = current_time after __init__ (its next_request(), :267)
+ *   step : the 4 draws of next_request() (:1132-1133, :1116, :1120)
+ *   reset: uniform(1,100,size=E) (:328), Z(Z-1) topology integers in loop order
+ *          (:331-338), per node (type, zone) (:350-354) and cpu (:373), endpoint hosts
+ *          (:380), then next_request()'s 4 draws (:397).  Only envs being reset read it.
+ */
+typedef struct lb_trace {
+    const double* t0;            /* [B]          */
+    const double* step_x1;       /* [B] exponential(1/arrival_rate) */
+    const double* step_x2;       /* [B] exponential(call_duration)  */
+    const int32_t* step_r;       /* [B] integers(0,7)               */
+    const int32_t* step_n;       /* [B] integers(0,num_nodes)       */
+    const double* reset_lat0;    /* [B*E]        */
+    const int32_t* reset_topo;   /* [B*Z*(Z-1)]  */
+    const int32_t* reset_ntype;  /* [B*N]        */
+    const int32_t* reset_nzone;  /* [B*N]        */
+    const int32_t* reset_ncpu;   /* [B*N]        */
+    const int32_t* reset_enode;  /* [B*E]        */
+    const double* reset_x1;      /* [B]          */
+    const double* reset_x2;      /* [B]          */
+    const int32_t* reset_r;      /* [B]          */
+    const int32_t* reset_n;      /* [B]          */
+} lb_trace;
+
+int lb_abi_version(void);
+const char* lb_last_error(void);
+
+/* Validate a configuration (reference constructor constraints). 0 = ok. */
+int lb_validate_config(const lb_config* cfg);
+
+/* Bytes of the opaque device state blob for num_envs envs (replaces the per-env
+ * Python object state of LoadBalancerK8sEnv.__init__, :86-287). */
+int lb_state_bytes(const lb_config* cfg, int64_t num_envs, uint64_t* out_bytes);
+
+/* LoadBalancerK8sEnv.__init__ (:86-287) for all envs: lookup tables, zeroed
+ * counters, current_time (the only init state that reaches reset()). */
+int lb_init(void* state, const lb_config* cfg, int64_t num_envs, const lb_trace* trace, void* stream);
+
+/* reset() (:290-400) for envs with reset_mask[b] != 0 (NULL = all); writes their
+ * obs rows [B, R, 8] float32 (R = E + rejection_allowed). */
+int lb_reset(void* state, const lb_config* cfg, int64_t num_envs, const uint8_t* reset_mask,
+             float* obs_out, const lb_trace* trace, void* stream);
+
+/* step(action) (:403-513) for all envs.  actions [B] int32 (Python semantics:
+ * -E..-1 wrap, E = reject, > E unrecognised/stale).  Outputs: obs [B,R,8] f32,
+ * reward [B] f32, done [B] u8; with cfg.auto_reset, envs that finish are reset in
+ * the same launch and their pre-reset obs go to terminal_obs_out (may be NULL) and
+ * their accumulators to ep_stats_out [B, LB_ST_K] f64 (may be NULL). */
+int lb_step(void* state, const lb_config* cfg, int64_t num_envs, const int32_t* actions,
+            float* obs_out, float* reward_out, uint8_t* done_out, float* terminal_obs_out,
+            double* ep_stats_out, const lb_trace* trace, void* stream);
+
+/* Batched envs/baselines.py policies (and uniform random) on the current state. */
+int lb_policy(const void* state, const lb_config* cfg, int64_t num_envs, int32_t kind,
+              int32_t* actions_out, void* stream);
+
+/* Materialise one env attribute (LB_FIELD_*) as float64 [B,E] or [B]. */
+int lb_get_field(const void* state, const lb_config* cfg, int64_t num_envs, int32_t field,
+                 double* out, void* stream);
+
+/* Current accumulators of every env as [B, LB_ST_K] float64 (per-step info). */
+int lb_get_stats(const void* state, const lb_config* cfg, int64_t num_envs, double* stats_out,
+                 void* stream);
+
+/* OR of LB_STATUS_* flags over all envs, written to *flags_out (device uint32). */
+int lb_status(const void* state, const lb_config* cfg, int64_t num_envs, uint32_t* flags_out,
+              void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LBK8S_H */

@@ -101,14 +101,14 @@ def replay(d, backend, check_state=True, n_steps=None, policy=None):
             _ = (ST_RETURN, ST_SUM_COST, ST_SUM_TOPO)
         if check_state and rt is None:
             f = backend.fields()
-            _eq("ep_lat", f["ep_lat"], d["state_ep_lat"][:, s], where)
-            _eq("ep_cpu", f["ep_cpu"], d["state_ep_cpu"][:, s], where)
-            _eq("ep_topo", f["ep_topo"], d["state_ep_topo"][:, s], where)
-            _eq("loads", f["loads"], d["state_loads"][:, s], where)
-            _eq("t", f["t"], d["state_t"][:, s], where)
-            _eq("dt", f["dt"], d["state_dt"][:, s], where)
-            _eq("req_zone", f["req_zone"], d["state_req"][:, s, 0], where)
-            _eq("req_thr", f["req_thr"], d["state_req"][:, s, 1], where)
+            exp = dict(ep_lat=d["state_ep_lat"][:, s], ep_cpu=d["state_ep_cpu"][:, s],
+                       ep_topo=d["state_ep_topo"][:, s], ep_cap=d["state_ep_cap"][:, s],
+                       ep_zone=d["state_ep_zone"][:, s], ep_node=d["state_ep_node"][:, s],
+                       loads=d["state_loads"][:, s], t=d["state_t"][:, s], dt=d["state_dt"][:, s],
+                       step=d["state_counters"][:, s, 0], req_zone=d["state_req"][:, s, 0],
+                       req_thr=d["state_req"][:, s, 1])
+            for key, val in f.items():
+                _eq(key, val, exp[key], where)
         counts["steps"] += 1
         counts["obs_values"] += exp_obs.size
     return counts

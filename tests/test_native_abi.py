@@ -1,0 +1,74 @@
+"""CPU-side checks of the C-ABI library (no GPU needed, no compute calls).
+
+* liblbk8s.so loads and exports every function include/lbk8s.h declares;
+* the ctypes structs match the header's field order (spot-checked by size);
+* host-only entry points (config validation, state sizing) behave like the
+  reference's constructor constraints.
+"""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "lbk8s.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(lb_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declares_expected_api():
+    fns = declared_functions()
+    for f in ("lb_init", "lb_reset", "lb_step", "lb_policy", "lb_state_bytes", "lb_last_error"):
+        assert f in fns
+
+
+def test_library_exports_every_declared_symbol():
+    from lbk8s import _native
+    L = _native.lib()
+    for f in declared_functions():
+        assert hasattr(L, f), f"{f} declared in include/lbk8s.h but not exported"
+    assert set(declared_functions()) == set(_native.EXPORTED_SYMBOLS)
+    assert L.lb_abi_version() == _native.ABI_VERSION
+
+
+def test_struct_sizes_match_header_layout():
+    from lbk8s import _native
+    # 8 x int32 + 5 x double + uint64 + int64 = 32 + 40 + 16
+    assert C.sizeof(_native.LBConfigC) == 88
+    assert C.sizeof(_native.LBTraceC) == 15 * 8
+
+
+def test_validate_and_state_bytes_host_only():
+    from lbk8s import LBConfig, _native
+    L = _native.lib()
+    c = LBConfig().to_c()
+    assert L.lb_validate_config(C.byref(c)) == 0
+    n = C.c_uint64()
+    assert L.lb_state_bytes(C.byref(c), 1 << 20, C.byref(n)) == 0
+    # ~E*16 + ~100 bytes per env plus the lookup tables
+    assert 100 * (1 << 20) < n.value < 400 * (1 << 20)
+    bad = LBConfig().to_c()
+    bad.num_nodes = 10
+    assert L.lb_validate_config(C.byref(bad)) != 0
+    assert b"IndexError" in L.lb_last_error()
+    with pytest.raises(IndexError):
+        _native.check(L.lb_validate_config(C.byref(bad)))
+
+
+def test_config_mirrors_reference_constructor_errors():
+    from lbk8s import LBConfig
+    with pytest.raises(IndexError):
+        LBConfig(num_nodes=12)
+    with pytest.raises(IndexError):
+        LBConfig(num_zones=3)
+    with pytest.raises(TypeError):
+        LBConfig(reward_function="bogus")
+    c = LBConfig(num_endpoints=6, rejection_allowed=False)
+    assert c.observation_space().shape == (6, 8)
+    assert c.action_space().n == 6
+    assert LBConfig().observation_space().shape == (9, 8)
