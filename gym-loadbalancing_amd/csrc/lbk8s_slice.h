@@ -1,0 +1,390 @@
+// lbk8s_slice.h — the "slice" path for E > 8 endpoints (e.g. the 64-endpoint
+// deep-sets scenario): one env = one W-lane slice of a wave (W = 16, 32 or 64), a lane
+// owns endpoint(s) e = lane + k*W, k < EPL.  Each lane writes its own 32-byte obs rows,
+// so a slice's stores cover the env's contiguous R x 32-byte block.  Per-env scalars are
+// loaded by every lane (same-address loads coalesce) and stored by lane 0; the three
+// Philox blocks of a request are computed by lanes 0/1/2 in one instruction stream.
+// Endpoint arrays are [env][EP] (es = 1, ee = EP).
+#pragma once
+
+#include "lbk8s_common.h"
+
+namespace lbk {
+
+template <int W>
+__device__ __forceinline__ int slice_sum(int v) {
+#pragma unroll
+    for (int m = W / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, W);
+    return v;
+}
+template <int W>
+__device__ __forceinline__ uint64_t slice_sum64(uint64_t v) {
+#pragma unroll
+    for (int m = W / 2; m >= 1; m >>= 1) {
+        uint32_t lo = __shfl_xor((uint32_t)v, m, W), hi = __shfl_xor((uint32_t)(v >> 32), m, W);
+        v += ((uint64_t)hi << 32) | lo;
+    }
+    return v;
+}
+template <int W>
+__device__ __forceinline__ uint64_t slice_or64(uint64_t v) {
+#pragma unroll
+    for (int m = W / 2; m >= 1; m >>= 1) {
+        uint32_t lo = __shfl_xor((uint32_t)v, m, W), hi = __shfl_xor((uint32_t)(v >> 32), m, W);
+        v |= ((uint64_t)hi << 32) | lo;
+    }
+    return v;
+}
+template <int W>
+__device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src, W); }
+template <int W>
+__device__ __forceinline__ double shfl_f64(double v, int src) { return __shfl(v, src, W); }
+
+template <int EPL, typename T>
+__device__ __forceinline__ T sel(const T (&a)[EPL], int k) {
+    T v = a[0];
+#pragma unroll
+    for (int i = 1; i < EPL; ++i)
+        if (k == i) v = a[i];
+    return v;
+}
+
+// next_request()'s draws (:1132-1133, :1116, :1120).  Draw map: block (D_REQ_X) ->
+// x1 from words (0,1), x2 from (2,3); block (D_REQ_I) -> r from word 0, n from word 1.
+// Lanes 0 and 1 compute the X block, lane 2 the I block; lanes 0/1 each take one log.
+template <int W, bool TRACE>
+__device__ __forceinline__ void slice_request_draws(const Params& p, int64_t env, uint32_t episode,
+                                                    uint32_t slot, int lane, bool from_reset, double& x1,
+                                                    double& x2, int& r, int& n) {
+    if constexpr (TRACE) {
+        if (from_reset) {
+            x1 = p.tr.reset_x1[env]; x2 = p.tr.reset_x2[env]; r = p.tr.reset_r[env]; n = p.tr.reset_n[env];
+        } else {
+            x1 = p.tr.step_x1[env]; x2 = p.tr.step_x2[env]; r = p.tr.step_r[env]; n = p.tr.step_n[env];
+        }
+    } else {
+        const int role = lane & 3;
+        U4 w = draw(p, env, episode, slot, role == 2 ? D_REQ_I : D_REQ_X);
+        double e = role == 1 ? std_exp(w.z, w.w) : std_exp(w.x, w.y);
+        x1 = p.inv_rate * shfl_f64<W>(e, 0);
+        x2 = p.call * shfl_f64<W>(e, 1);
+        r = (int)bounded(shfl_u32<W>(w.x, 2), 7);
+        n = (int)bounded(shfl_u32<W>(w.y, 2), (uint32_t)p.N);
+    }
+}
+
+// Register image of one env slice.
+template <int EPL>
+struct SEnv {
+    double lat0[EPL];
+    uint32_t em[EPL], ed[EPL];
+    float olat[EPL], ocpu[EPL];  // observed endpoint latency / cpu (float32 obs columns 4, 2)
+    double t, dt, sum_lat, sum_cpu, total, last_r;
+    uint64_t topo, zcap, acc2, acc3;
+    uint64_t nz0, nz1;  // node-zone words 0 and 1 (nodes < 64), prefetched with the state
+    Scal s;
+};
+
+// get_state() (:688-758): rows [zone, zone_cpu_cap, cpu, topo_lat, lat, req_zone, thr, dt]
+template <int W, int EPL>
+__device__ __forceinline__ void slice_write_obs(const Params& p, float* out, int64_t env, int lane,
+                                                const SEnv<EPL>& v) {
+    float* base = out + env * (int64_t)p.R * 8;
+    const float rz = (float)v.s.rz, thr = (float)threshold(v.s.thr_idx), dt = (float)v.dt;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+        int e = lane + k * W;
+        if (e < p.E) {
+            int z = em_zone(v.em[k]);
+            float4 a = make_float4((float)z, (float)zcap_val(v.zcap, z), v.ocpu[k],
+                                   (float)topo_val(v.topo, z, v.s.rz));
+            float4 b = make_float4(v.olat[k], rz, thr, dt);
+            float4* row = reinterpret_cast<float4*>(base + e * 8);
+            row[0] = a;
+            row[1] = b;
+        }
+    }
+    if (p.rejection && lane == (p.E % W)) {
+        float4* row = reinterpret_cast<float4*>(base + p.E * 8);
+        row[0] = make_float4(-1.f, -1.f, -1.f, -1.f);
+        row[1] = make_float4(-1.f, rz, thr, dt);
+    }
+}
+
+template <int W, int EPL>
+__device__ __forceinline__ void slice_load(const Params& p, int64_t env, int lane, SEnv<EPL>& v) {
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+        int64_t i = eidx(p, env, lane + k * W);
+        v.lat0[k] = p.lat0[i];
+        v.em[k] = p.emeta[i];
+        v.ed[k] = p.edyn[i];
+    }
+    v.t = p.t[env];
+    v.s = sc_unpack(p.sc[env]);
+    v.topo = p.topo[env];
+    v.zcap = p.zcap[env];
+    v.nz0 = p.nzone[env];
+    v.nz1 = p.NZW > 1 ? p.nzone[p.B + env] : 0;
+    v.acc2 = p.acc2[env];
+    v.acc3 = p.acc3[env];
+    v.sum_lat = p.sum_lat[env];
+    v.sum_cpu = p.sum_cpu[env];
+    v.total = p.total[env];
+    v.last_r = p.reward_fn != LB_REWARD_NAIVE ? p.last_r[env] : 0.0;
+}
+
+template <int EPL>
+__device__ __forceinline__ void slice_store_scalars(const Params& p, int64_t env, const SEnv<EPL>& v) {
+    p.t[env] = v.t;
+    p.sc[env] = sc_pack(v.s);
+    p.acc2[env] = v.acc2;
+    p.acc3[env] = v.acc3;
+    p.sum_lat[env] = v.sum_lat;
+    p.sum_cpu[env] = v.sum_cpu;
+    p.total[env] = v.total;
+    if (p.reward_fn != LB_REWARD_NAIVE) p.last_r[env] = v.last_r;
+}
+
+// the request part of next_request() (:1131-1163); the dequeue part is folded into the LUTs
+template <int W, bool TRACE, int EPL>
+__device__ __forceinline__ void slice_next_request(const Params& p, int64_t env, int lane, bool from_reset,
+                                                   SEnv<EPL>& v) {
+    double x1, x2;
+    int r, n;
+    slice_request_draws<W, TRACE>(p, env, (uint32_t)(v.acc3 >> 32), (uint32_t)v.s.step, lane, from_reset,
+                                  x1, x2, r, n);
+    double arrival = v.t + x1;
+    double departure = arrival + x2;
+    v.dt = departure - arrival;
+    v.t = arrival;
+    v.s.thr_idx = (r + 6) % 7;  // endpoint_list[r - 1] (:1117)
+    uint64_t word = n < 32 ? v.nz0 : (n < 64 ? v.nz1 : p.nzone[(n >> 5) * p.B + env]);
+    v.s.rz = (int)((word >> (2 * (n & 31))) & 3);
+}
+
+// reset() (:290-400) into registers, then the per-episode state stores.
+template <int W, int EPL, bool TRACE>
+__device__ void slice_reset(const Params& p, int64_t env, int lane, SEnv<EPL>& v) {
+    const uint32_t episode = (uint32_t)(v.acc3 >> 32) + 1;
+    // nodes (:349-373): zone capacity and the 2-bit zone of every node, one 32-node word
+    // at a time (lane l takes nodes l, l+W, ... of the word)
+    uint64_t zc = 0;
+    for (int w = 0; w < p.NZW; ++w) {
+        uint64_t word = 0;
+        for (int n = 32 * w + lane; n < 32 * (w + 1) && n < p.N; n += W) {
+            int ty, zo, cpu;
+            node_draw<TRACE>(p, env, episode, n, ty, zo, cpu);
+            zc += (uint64_t)node_cpu_int(ty) << (16 * zo);
+            word |= (uint64_t)zo << (2 * (n & 31));
+        }
+        word = slice_or64<W>(word);
+        if (w == 0) v.nz0 = word;
+        if (w == 1) v.nz1 = word;
+        if (lane == 0) p.nzone[w * p.B + env] = word;
+    }
+    if (p.NZW < 2) v.nz1 = 0;
+    zc = slice_sum64<W>(zc);
+    // endpoints (:328, :379-386)
+    int node[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+        int e = lane + k * W;
+        node[k] = 0;
+        v.lat0[k] = 0.0;
+        if (e < p.E) {
+            if constexpr (TRACE) {
+                v.lat0[k] = p.tr.reset_lat0[env * p.E + e];
+                node[k] = p.tr.reset_enode[env * p.E + e];
+            } else {
+                U4 w = draw(p, env, episode, (uint32_t)e, D_EP);
+                v.lat0[k] = 1.0 + 99.0 * u53(w.x, w.y);
+                node[k] = (int)bounded(w.z, 24);
+            }
+        }
+    }
+    // owner slot = first endpoint hosted on the same node (shares that node's CPU)
+    int owner[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) owner[k] = lane + k * W;
+    for (int e2 = 0; e2 < p.E; ++e2) {
+        int nd2 = shfl_u32<W>((uint32_t)sel<EPL>(node, e2 / W), e2 % W);
+#pragma unroll
+        for (int k = 0; k < EPL; ++k)
+            if (nd2 == node[k] && e2 < owner[k]) owner[k] = e2;
+    }
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+        int e = lane + k * W;
+        v.em[k] = 0;
+        v.ed[k] = 0;
+        v.olat[k] = 0.f;
+        v.ocpu[k] = 0.f;
+        if (e < p.E) {
+            int ty, zo, cpu;
+            node_draw<TRACE>(p, env, episode, node[k], ty, zo, cpu);
+            v.em[k] = em_pack(zo, owner[k], ty, cpu, node[k]);
+            v.olat[k] = (float)v.lat0[k];
+            v.ocpu[k] = (float)cpu;
+        }
+        int64_t i = eidx(p, env, e);
+        p.lat0[i] = v.lat0[k];
+        p.emeta[i] = v.em[k];
+        p.edyn[i] = 0;
+    }
+    // topology (:331-338): symmetric, diag 1; the 4x4 zone block is all that is observable
+    uint64_t topo = 0;
+    if constexpr (TRACE) {
+        const int32_t* d = p.tr.reset_topo + env * (int64_t)p.Z * (p.Z - 1);
+        int q = 0;
+        for (int i = 0; i < 4; ++i)
+            for (int j = i + 1; j < 4; ++j, ++q)  // last writer: (z1=j, z2=i)
+                topo |= (uint64_t)(d[j * (p.Z - 1) + i] & 0x1FF) << (9 * q);
+    } else {
+        U4 a = draw(p, env, episode, 0, D_TOPO), b = draw(p, env, episode, 1, D_TOPO);
+        topo = (uint64_t)(1 + bounded(a.x, 499)) | ((uint64_t)(1 + bounded(a.y, 499)) << 9) |
+               ((uint64_t)(1 + bounded(a.z, 499)) << 18) | ((uint64_t)(1 + bounded(a.w, 499)) << 27) |
+               ((uint64_t)(1 + bounded(b.x, 499)) << 36) | ((uint64_t)(1 + bounded(b.y, 499)) << 45);
+    }
+    v.topo = topo;
+    v.zcap = zc;
+    v.acc2 = 0;
+    v.acc3 = (uint64_t)episode << 32;
+    v.sum_lat = 0.0;
+    v.sum_cpu = 0.0;
+    v.total = 0.0;
+    v.last_r = p.init_last_r;
+    v.s.step = 0; v.s.acc = 0; v.s.intra = 0; v.s.penalty = 0; v.s.reset_done = 1;
+    slice_next_request<W, TRACE, EPL>(p, env, lane, true, v);
+    if (lane == 0) {
+        p.topo[env] = topo;
+        p.zcap[env] = zc;
+    }
+}
+
+template <int W, int EPL, bool TRACE>
+__global__ __launch_bounds__(BLOCK) void k_reset_slice(Params p) {
+    const int lane = threadIdx.x % W;
+    const int64_t env = (int64_t)blockIdx.x * (BLOCK / W) + threadIdx.x / W;
+    if (env >= p.B) return;
+    if (p.reset_mask && !p.reset_mask[env]) return;
+    SEnv<EPL> v;
+    v.t = p.t[env];
+    v.acc3 = p.acc3[env];
+    v.s = sc_unpack(p.sc[env]);
+    slice_reset<W, EPL, TRACE>(p, env, lane, v);
+    if (p.obs) slice_write_obs<W, EPL>(p, p.obs, env, lane, v);
+    if (lane == 0) slice_store_scalars<EPL>(p, env, v);
+}
+
+// step() (:403-513) fused with next_request(), get_state(), reward, done and auto-reset.
+template <int W, int EPL, bool TRACE>
+__global__ __launch_bounds__(BLOCK) void k_step_slice(Params p) {
+    const int lane = threadIdx.x % W;
+    const int64_t env = (int64_t)blockIdx.x * (BLOCK / W) + threadIdx.x / W;
+    if (env >= p.B) return;
+    const int E = p.E;
+    // ---- phase 0: independent loads (state + action)
+    SEnv<EPL> v;
+    slice_load<W, EPL>(p, env, lane, v);
+    const int a = p.actions[env];
+
+    // ---- phase 1: decode, then every table lookup the step needs, issued together
+    v.s.step = v.s.step < 0xFFFF ? v.s.step + 1 : 0xFFFF;
+    const bool accept = a >= -E && a < E;
+    const bool reject = a == E;
+    if (a < -E) v.s.bad = 1;  // reference: IndexError; here: treated as unrecognised
+    if (!v.s.reset_done) v.s.bad = 1;
+    const int ai = accept ? (a < 0 ? a + E : a) : 0;
+    const int src = ai % W, sk = ai / W;
+    const uint32_t emA = shfl_u32<W>(sel<EPL>(v.em, sk), src);
+    const uint32_t edA = shfl_u32<W>(sel<EPL>(v.ed, sk), src);
+    const double lat0A = shfl_f64<W>(sel<EPL>(v.lat0, sk), src);
+    const int oA = em_owner(emA);
+    const uint32_t edO = shfl_u32<W>(sel<EPL>(v.ed, oA / W), oA % W);
+    const int jA = ed_j(edA);
+    const int Mn = ed_M(edO) < CMAX ? ed_M(edO) + 1 : CMAX;
+    const int jn = jA < CMAX ? jA + 1 : CMAX;
+    const int k0A = (int)lat0A, c0A = em_c0(emA);
+    // selected endpoint before (selected_*) and after (inc+dec) this step's update
+    const double lut_selA = p.lat_lut[k0A * JCAP + jA];
+    const double sel_cpu = p.cpu_lut[c0A * JCAP + ed_m(edA)];
+    const double next_lat = p.lat_lut[k0A * JCAP + jn];
+    const double next_cpu = p.cpu_lut[c0A * JCAP + Mn];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {  // observed values of every endpoint
+        const double l = p.lat_lut[(int)v.lat0[k] * JCAP + ed_j(v.ed[k])];
+        v.olat[k] = (float)(ed_j(v.ed[k]) == 0 ? v.lat0[k] : l);
+        v.ocpu[k] = (float)p.cpu_lut[em_c0(v.em[k]) * JCAP + ed_m(v.ed[k])];
+    }
+
+    // ---- take_action (:578-686)
+    double reward;
+    if (accept) {
+        const int zA = em_zone(emA);
+        const double sel_lat = jA == 0 ? lat0A : lut_selA;
+        const int tl = topo_val(v.topo, v.s.rz, zA);
+        // O(E) Gini numerator update for avg_load_served[ai] += 1 (:631)
+        int cnt = 0;
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) {
+            int e = lane + k * W;
+            if (e < E && e != ai && ed_j(v.ed[k]) <= jA) ++cnt;
+        }
+        cnt = slice_sum<W>(cnt);
+        uint32_t gnum = (uint32_t)(v.acc2 >> 32) + (uint32_t)(2 * (2 * cnt - (E - 1)));
+        uint32_t sum_topo = (uint32_t)v.acc2 + (uint32_t)tl;
+        v.acc2 = ((uint64_t)gnum << 32) | sum_topo;
+        v.acc3 += (uint64_t)node_cost(em_type(emA));
+        v.s.acc = v.s.acc < 0xFFFF ? v.s.acc + 1 : 0xFFFF;
+        if (v.s.rz == zA) v.s.intra = v.s.intra < 0xFFFF ? v.s.intra + 1 : 0xFFFF;
+        v.sum_lat += sel_lat;
+        v.sum_cpu += sel_cpu;
+        // increase_resources / increase_endpoint_latency (:674-677) and the same step's
+        // decrease in next_request() (:1137-1143) -> the history counters advance
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) {
+            int e = lane + k * W;
+            if (e == oA) v.ed[k] = (v.ed[k] & ~(0x3FFu << 20)) | ((uint32_t)Mn << 20);
+            if (e == ai) {
+                v.ed[k] = (v.ed[k] & (0x3FFu << 20)) | ((uint32_t)Mn << 10) | (uint32_t)jn;
+                v.olat[k] = (float)next_lat;
+                v.ocpu[k] = (float)next_cpu;
+            }
+        }
+        v.s.penalty = 0;
+        reward = accept_reward(p, sel_lat, tl, sel_cpu, v.acc2, v.s.acc);
+        v.last_r = reward;
+    } else if (reject) {
+        v.s.penalty = 1;
+        reward = p.reward_fn == LB_REWARD_LATENCY ? -1000.0 : -1.0;
+        v.last_r = reward;
+    } else {  // unrecognised action (:685-686): penalty and selected_* stay stale
+        reward = p.reward_fn == LB_REWARD_NAIVE ? (v.s.penalty ? -1.0 : 1.0) : v.last_r;
+    }
+    v.total += reward;
+
+    // ---- next_request (:1131-1163), done (:472), outputs
+    slice_next_request<W, TRACE, EPL>(p, env, lane, false, v);
+    const bool done = v.s.step == p.L;
+    if (lane == 0) {
+        if (p.reward) p.reward[env] = (float)reward;
+        if (p.done) p.done[env] = (uint8_t)done;
+    }
+    if (done && p.auto_reset) {
+        if (p.term_obs) slice_write_obs<W, EPL>(p, p.term_obs, env, lane, v);
+        if (p.ep_stats && lane == 0)
+            write_stats_row(p, p.ep_stats + env * LB_ST_K, v.s, v.acc2, v.acc3, v.total, v.sum_lat, v.sum_cpu);
+        slice_reset<W, EPL, TRACE>(p, env, lane, v);
+    } else if (accept) {
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) {
+            int e = lane + k * W;
+            if (e == ai || e == oA) p.edyn[eidx(p, env, e)] = v.ed[k];
+        }
+    }
+    if (p.obs) slice_write_obs<W, EPL>(p, p.obs, env, lane, v);
+    if (lane == 0) slice_store_scalars<EPL>(p, env, v);
+}
+
+}  // namespace lbk

@@ -1,0 +1,378 @@
+// lbk8s_tpe.h — the thread-per-env path for E <= 8 endpoints (the default 8-endpoint
+// scenario and run_baselines' 6-endpoint one).
+//
+// One lane = one env: the per-env scalar work (Philox draws, the float64 log of the
+// exponential draws, reward, accumulators) runs once per env instead of once per
+// endpoint lane, and every state load/store is a fully coalesced 64-lane access of the
+// endpoint-major SoA layout (endpoint arrays are [E][B]: es = B, ee = 1).
+//
+// Observations: each lane writes a compact image of its env (29 words: per endpoint
+// {zone|cap, cpu f32, lat f32}, plus req zone/threshold, dt, topology) into LDS; the
+// wave then copies its 64 envs' (R x 8) float32 rows out as contiguous float4 runs
+// (tpe_copy_out), so the 288-byte-per-env obs stream leaves the CU as full cache lines
+// instead of 64 scattered 16-byte pieces per store instruction.
+#pragma once
+
+#include "lbk8s_common.h"
+
+namespace lbk {
+
+// image words: [0] rz | thr_idx<<2 | flag<<5   [1] f32 dt   [2],[3] topology lo/hi
+//              [4+3e] zone | cap<<2   [5+3e] f32 cpu   [6+3e] f32 latency
+constexpr int TPE_CW = 4 + 3 * TPE_E + 1;  // 29: odd stride -> conflict-free per-lane writes
+constexpr int TPE_FLAG = 1 << 5;
+
+struct TEnv {
+    double t, dt, sum_lat, sum_cpu, total, last_r;
+    uint64_t topo, zcap, acc2, acc3, nz0, nz1;
+    Scal s;
+};
+
+template <bool TRACE>
+__device__ __forceinline__ void tpe_request_draws(const Params& p, int64_t env, uint32_t episode,
+                                                  uint32_t slot, bool from_reset, double& x1, double& x2,
+                                                  int& r, int& n) {
+    if constexpr (TRACE) {
+        if (from_reset) {
+            x1 = p.tr.reset_x1[env]; x2 = p.tr.reset_x2[env]; r = p.tr.reset_r[env]; n = p.tr.reset_n[env];
+        } else {
+            x1 = p.tr.step_x1[env]; x2 = p.tr.step_x2[env]; r = p.tr.step_r[env]; n = p.tr.step_n[env];
+        }
+    } else {  // draw map: (D_REQ_X) -> x1 words 0,1 / x2 words 2,3; (D_REQ_I) -> r word 0 / n word 1
+        U4 a = draw(p, env, episode, slot, D_REQ_X);
+        U4 b = draw(p, env, episode, slot, D_REQ_I);
+        x1 = p.inv_rate * std_exp(a.x, a.y);
+        x2 = p.call * std_exp(a.z, a.w);
+        r = (int)bounded(b.x, 7);
+        n = (int)bounded(b.y, (uint32_t)p.N);
+    }
+}
+
+__device__ __forceinline__ void tpe_image_env(uint32_t* me, const TEnv& v, int flag) {
+    me[0] = (uint32_t)v.s.rz | ((uint32_t)v.s.thr_idx << 2) | (uint32_t)flag;
+    me[1] = __float_as_uint((float)v.dt);
+    me[2] = (uint32_t)v.topo;
+    me[3] = (uint32_t)(v.topo >> 32);
+}
+
+// get_state() (:688-758) for the wave's envs: rows [zone, cap, cpu, topo, lat, rz, thr, dt],
+// plus the reject row [-1 x 5, rz, thr, dt].  flagged: only envs whose image flag is set.
+__device__ __forceinline__ void tpe_copy_out(const Params& p, float* out, const uint32_t* img,
+                                             int64_t env0, bool flagged) {
+    const int lane = threadIdx.x & 63;
+    const int P = 2 * p.R;  // float4 pieces per env (<= 18)
+    const int G = 64 / P;   // envs per store instruction
+    const int eo = lane / P, piece = lane - eo * P;
+    if (eo >= G) return;
+    const int row = piece >> 1, half = piece & 1;
+    const int64_t left = p.B - env0;
+    const int nenv = left < 64 ? (int)left : 64;
+    for (int el = eo; el < nenv; el += G) {
+        const uint32_t* c = img + el * TPE_CW;
+        const uint32_t w0 = c[0];
+        if (flagged && !(w0 & TPE_FLAG)) continue;
+        const int rz = (int)(w0 & 3);
+        const float thr = (float)threshold((int)((w0 >> 2) & 7));
+        const float dt = __uint_as_float(c[1]);
+        float4 v;
+        if (row < p.E) {
+            if (half == 0) {
+                const uint32_t q = c[4 + 3 * row];
+                const int z = (int)(q & 3);
+                const uint64_t topo = (uint64_t)c[2] | ((uint64_t)c[3] << 32);
+                v = make_float4((float)z, (float)(q >> 2), __uint_as_float(c[5 + 3 * row]),
+                                (float)topo_val(topo, z, rz));
+            } else {
+                v = make_float4(__uint_as_float(c[6 + 3 * row]), (float)rz, thr, dt);
+            }
+        } else {
+            v = half == 0 ? make_float4(-1.f, -1.f, -1.f, -1.f) : make_float4(-1.f, (float)rz, thr, dt);
+        }
+        reinterpret_cast<float4*>(out + (env0 + el) * (int64_t)p.R * 8)[piece] = v;
+    }
+}
+
+// reset() (:290-400) for this lane's env: draws, per-episode state stores, image.
+template <bool TRACE>
+__device__ void tpe_reset(const Params& p, int64_t env, TEnv& v, uint32_t* me) {
+    const int E = p.E;
+    const uint32_t episode = (uint32_t)(v.acc3 >> 32) + 1;
+    // next_request() closing reset() (:397), drawn first: its node's zone is captured
+    // while the node words are built (Philox is counter-based; trace values are given)
+    double x1, x2;
+    int r, n;
+    tpe_request_draws<TRACE>(p, env, episode, 0, true, x1, x2, r, n);
+    // nodes (:349-373): zone capacity + 2-bit zone words
+    uint64_t zc = 0, nzq = 0;
+    v.nz0 = 0;
+    v.nz1 = 0;
+    for (int w = 0; w < p.NZW; ++w) {
+        uint64_t word = 0;
+        const int nend = 32 * (w + 1) < p.N ? 32 * (w + 1) : p.N;
+        for (int k = 32 * w; k < nend; ++k) {
+            int ty, zo, cpu;
+            node_draw<TRACE>(p, env, episode, k, ty, zo, cpu);
+            zc += (uint64_t)node_cpu_int(ty) << (16 * zo);
+            word |= (uint64_t)zo << (2 * (k & 31));
+        }
+        if (w == 0) v.nz0 = word;
+        if (w == 1) v.nz1 = word;
+        if (w == (n >> 5)) nzq = word;
+        p.nzone[w * p.B + env] = word;
+    }
+    // endpoints (:328, :379-386)
+    double lat0[TPE_E];
+    int node[TPE_E];
+#pragma unroll
+    for (int e = 0; e < TPE_E; ++e) {
+        lat0[e] = 0.0;
+        node[e] = 0;
+        if (e < E) {
+            if constexpr (TRACE) {
+                lat0[e] = p.tr.reset_lat0[env * E + e];
+                node[e] = p.tr.reset_enode[env * E + e];
+            } else {
+                U4 w = draw(p, env, episode, (uint32_t)e, D_EP);
+                lat0[e] = 1.0 + 99.0 * u53(w.x, w.y);
+                node[e] = (int)bounded(w.z, 24);
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < TPE_E; ++e) {
+        if (e < E) {
+            int owner = e;  // first endpoint hosted on the same node (shares its cpu)
+#pragma unroll
+            for (int e2 = TPE_E - 1; e2 >= 0; --e2)
+                if (e2 < e && node[e2] == node[e]) owner = e2;
+            int ty, zo, cpu;
+            node_draw<TRACE>(p, env, episode, node[e], ty, zo, cpu);
+            const int64_t i = (int64_t)e * p.B + env;
+            p.lat0[i] = lat0[e];
+            p.emeta[i] = em_pack(zo, owner, ty, cpu, node[e]);
+            p.edyn[i] = 0;
+            me[4 + 3 * e] = (uint32_t)zo | ((uint32_t)zcap_val(zc, zo) << 2);
+            me[5 + 3 * e] = __float_as_uint((float)cpu);
+            me[6 + 3 * e] = __float_as_uint((float)lat0[e]);
+        }
+    }
+    // topology (:331-338): symmetric, diag 1; the 4x4 zone block is all that is observable
+    uint64_t topo = 0;
+    if constexpr (TRACE) {
+        const int32_t* d = p.tr.reset_topo + env * (int64_t)p.Z * (p.Z - 1);
+        int q = 0;
+        for (int i = 0; i < 4; ++i)
+            for (int j = i + 1; j < 4; ++j, ++q)  // last writer: (z1=j, z2=i)
+                topo |= (uint64_t)(d[j * (p.Z - 1) + i] & 0x1FF) << (9 * q);
+    } else {
+        U4 a = draw(p, env, episode, 0, D_TOPO), b = draw(p, env, episode, 1, D_TOPO);
+        topo = (uint64_t)(1 + bounded(a.x, 499)) | ((uint64_t)(1 + bounded(a.y, 499)) << 9) |
+               ((uint64_t)(1 + bounded(a.z, 499)) << 18) | ((uint64_t)(1 + bounded(a.w, 499)) << 27) |
+               ((uint64_t)(1 + bounded(b.x, 499)) << 36) | ((uint64_t)(1 + bounded(b.y, 499)) << 45);
+    }
+    v.topo = topo;
+    v.zcap = zc;
+    v.acc2 = 0;
+    v.acc3 = (uint64_t)episode << 32;
+    v.sum_lat = 0.0;
+    v.sum_cpu = 0.0;
+    v.total = 0.0;
+    v.last_r = p.init_last_r;
+    v.s.step = 0; v.s.acc = 0; v.s.intra = 0; v.s.penalty = 0; v.s.reset_done = 1;
+    const double arrival = v.t + x1;
+    const double departure = arrival + x2;
+    v.dt = departure - arrival;
+    v.t = arrival;
+    v.s.thr_idx = (r + 6) % 7;
+    v.s.rz = (int)((nzq >> (2 * (n & 31))) & 3);
+    p.topo[env] = topo;
+    p.zcap[env] = zc;
+}
+
+__device__ __forceinline__ void tpe_store_scalars(const Params& p, int64_t env, const TEnv& v) {
+    p.t[env] = v.t;
+    p.sc[env] = sc_pack(v.s);
+    p.acc2[env] = v.acc2;
+    p.acc3[env] = v.acc3;
+    p.sum_lat[env] = v.sum_lat;
+    p.sum_cpu[env] = v.sum_cpu;
+    p.total[env] = v.total;
+    if (p.reward_fn != LB_REWARD_NAIVE) p.last_r[env] = v.last_r;
+}
+
+template <bool TRACE>
+__global__ __launch_bounds__(BLOCK) void k_reset_tpe(Params p) {
+    __shared__ uint32_t lds[BLOCK * TPE_CW];
+    const int lane = threadIdx.x & 63;
+    uint32_t* img = lds + (threadIdx.x & ~63) * TPE_CW;
+    uint32_t* me = img + lane * TPE_CW;
+    const int64_t env0 = (int64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63);
+    const int64_t env = env0 + lane;
+    const bool doit = env < p.B && (!p.reset_mask || p.reset_mask[env]);
+    me[0] = 0;
+    if (doit) {
+        TEnv v;
+        v.t = p.t[env];
+        v.acc3 = p.acc3[env];
+        v.s = sc_unpack(p.sc[env]);
+        tpe_reset<TRACE>(p, env, v, me);
+        tpe_image_env(me, v, TPE_FLAG);
+        tpe_store_scalars(p, env, v);
+    }
+    __syncthreads();
+    if (p.obs) tpe_copy_out(p, p.obs, img, env0, true);
+}
+
+// step() (:403-513) fused with next_request(), get_state(), reward, done and auto-reset.
+template <bool TRACE>
+__global__ __launch_bounds__(BLOCK) void k_step_tpe(Params p) {
+    __shared__ uint32_t lds[BLOCK * TPE_CW];
+    const int lane = threadIdx.x & 63;
+    uint32_t* img = lds + (threadIdx.x & ~63) * TPE_CW;
+    uint32_t* me = img + lane * TPE_CW;
+    const int64_t env0 = (int64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63);
+    const int64_t env = env0 + lane;
+    const bool live = env < p.B;
+    const int64_t ev = live ? env : 0;  // dead lanes read env 0 (harmless) and store nothing
+    const int E = p.E;
+
+    // ---- phase 0: every independent load, coalesced across the wave
+    TEnv v;
+    double lat0[TPE_E];
+    uint32_t em[TPE_E], ed[TPE_E];
+#pragma unroll
+    for (int e = 0; e < TPE_E; ++e) {
+        const int64_t i = (int64_t)e * p.B + ev;
+        lat0[e] = e < E ? p.lat0[i] : 0.0;
+        em[e] = e < E ? p.emeta[i] : 0u;
+        ed[e] = e < E ? p.edyn[i] : 0u;
+    }
+    const int a = p.actions[ev];
+    v.t = p.t[ev];
+    v.s = sc_unpack(p.sc[ev]);
+    v.topo = p.topo[ev];
+    v.zcap = p.zcap[ev];
+    v.nz0 = p.nzone[ev];
+    v.nz1 = p.NZW > 1 ? p.nzone[p.B + ev] : 0;
+    v.acc2 = p.acc2[ev];
+    v.acc3 = p.acc3[ev];
+    v.sum_lat = p.sum_lat[ev];
+    v.sum_cpu = p.sum_cpu[ev];
+    v.total = p.total[ev];
+    v.last_r = p.reward_fn != LB_REWARD_NAIVE ? p.last_r[ev] : 0.0;
+
+    // ---- phase 1: decode the action, pick the selected endpoint, table lookups
+    v.s.step = v.s.step < 0xFFFF ? v.s.step + 1 : 0xFFFF;
+    const bool accept = a >= -E && a < E;
+    const bool reject = a == E;
+    if (a < -E) v.s.bad = 1;  // reference: IndexError; here: treated as unrecognised
+    if (!v.s.reset_done) v.s.bad = 1;
+    const int ai = accept ? (a < 0 ? a + E : a) : 0;
+    uint32_t emA = em[0], edA = ed[0];
+    double lat0A = lat0[0];
+#pragma unroll
+    for (int e = 1; e < TPE_E; ++e)
+        if (ai == e) { emA = em[e]; edA = ed[e]; lat0A = lat0[e]; }
+    const int oA = em_owner(emA);
+    uint32_t edO = ed[0];
+#pragma unroll
+    for (int e = 1; e < TPE_E; ++e)
+        if (oA == e) edO = ed[e];
+    const int jA = ed_j(edA);
+    const int Mn = ed_M(edO) < CMAX ? ed_M(edO) + 1 : CMAX;
+    const int jn = jA < CMAX ? jA + 1 : CMAX;
+    const int k0A = (int)lat0A, c0A = em_c0(emA);
+    const double lut_selA = p.lat_lut[k0A * JCAP + jA];
+    const double sel_cpu = p.cpu_lut[c0A * JCAP + ed_m(edA)];
+    const double next_lat = p.lat_lut[k0A * JCAP + jn];
+    const double next_cpu = p.cpu_lut[c0A * JCAP + Mn];
+    int cnt = 0;  // #{e != ai : loads[e] <= loads[ai]} for the O(E) Gini update
+#pragma unroll
+    for (int e = 0; e < TPE_E; ++e) {
+        if (e < E) {
+            const int j = ed_j(ed[e]);
+            const double l = p.lat_lut[(int)lat0[e] * JCAP + j];
+            const double c = p.cpu_lut[em_c0(em[e]) * JCAP + ed_m(ed[e])];
+            float ol = j == 0 ? (float)lat0[e] : (float)l;
+            float oc = (float)c;
+            if (accept && e == ai) { ol = (float)next_lat; oc = (float)next_cpu; }
+            const int z = em_zone(em[e]);
+            me[4 + 3 * e] = (uint32_t)z | ((uint32_t)zcap_val(v.zcap, z) << 2);
+            me[5 + 3 * e] = __float_as_uint(oc);
+            me[6 + 3 * e] = __float_as_uint(ol);
+            if (e != ai && j <= jA) ++cnt;
+        }
+    }
+
+    // ---- take_action (:578-686)
+    double reward;
+    if (accept) {
+        const int zA = em_zone(emA);
+        const double sel_lat = jA == 0 ? lat0A : lut_selA;
+        const int tl = topo_val(v.topo, v.s.rz, zA);
+        const uint32_t gnum = (uint32_t)(v.acc2 >> 32) + (uint32_t)(2 * (2 * cnt - (E - 1)));
+        const uint32_t sum_topo = (uint32_t)v.acc2 + (uint32_t)tl;
+        v.acc2 = ((uint64_t)gnum << 32) | sum_topo;
+        v.acc3 += (uint64_t)node_cost(em_type(emA));
+        v.s.acc = v.s.acc < 0xFFFF ? v.s.acc + 1 : 0xFFFF;
+        if (v.s.rz == zA) v.s.intra = v.s.intra < 0xFFFF ? v.s.intra + 1 : 0xFFFF;
+        v.sum_lat += sel_lat;
+        v.sum_cpu += sel_cpu;
+        // increase_resources / increase_endpoint_latency (:674-677) and the same step's
+        // decrease in next_request() (:1137-1143) -> the history counters advance
+        const uint32_t edA_new = ((oA == ai ? (uint32_t)Mn : (uint32_t)ed_M(edA)) << 20) |
+                                 ((uint32_t)Mn << 10) | (uint32_t)jn;
+        if (live) {
+            if (oA != ai) p.edyn[(int64_t)oA * p.B + env] = (edO & ~(0x3FFu << 20)) | ((uint32_t)Mn << 20);
+            p.edyn[(int64_t)ai * p.B + env] = edA_new;
+        }
+        v.s.penalty = 0;
+        reward = accept_reward(p, sel_lat, tl, sel_cpu, v.acc2, v.s.acc);
+        v.last_r = reward;
+    } else if (reject) {
+        v.s.penalty = 1;
+        reward = p.reward_fn == LB_REWARD_LATENCY ? -1000.0 : -1.0;
+        v.last_r = reward;
+    } else {  // unrecognised action (:685-686): penalty and selected_* stay stale
+        reward = p.reward_fn == LB_REWARD_NAIVE ? (v.s.penalty ? -1.0 : 1.0) : v.last_r;
+    }
+    v.total += reward;
+
+    // ---- next_request (:1131-1163)
+    {
+        double x1, x2;
+        int r, n;
+        tpe_request_draws<TRACE>(p, ev, (uint32_t)(v.acc3 >> 32), (uint32_t)v.s.step, false, x1, x2, r, n);
+        const double arrival = v.t + x1;
+        const double departure = arrival + x2;
+        v.dt = departure - arrival;
+        v.t = arrival;
+        v.s.thr_idx = (r + 6) % 7;  // endpoint_list[r - 1] (:1117)
+        const uint64_t word = n < 32 ? v.nz0 : (n < 64 ? v.nz1 : p.nzone[(int64_t)(n >> 5) * p.B + ev]);
+        v.s.rz = (int)((word >> (2 * (n & 31))) & 3);
+    }
+    const bool done = live && v.s.step == p.L;  // (:472)
+    if (live) {
+        if (p.reward) p.reward[env] = (float)reward;
+        if (p.done) p.done[env] = (uint8_t)done;
+    }
+    tpe_image_env(me, v, done ? TPE_FLAG : 0);
+
+    // ---- VecEnv auto-reset: terminal obs + episode stats, then reset() (:290-400)
+    const bool do_reset = done && p.auto_reset;
+    if (__syncthreads_or(do_reset)) {
+        if (p.term_obs) tpe_copy_out(p, p.term_obs, img, env0, true);
+        if (do_reset && p.ep_stats)
+            write_stats_row(p, p.ep_stats + env * LB_ST_K, v.s, v.acc2, v.acc3, v.total, v.sum_lat, v.sum_cpu);
+        __syncthreads();
+        if (do_reset) {
+            tpe_reset<TRACE>(p, env, v, me);
+            tpe_image_env(me, v, 0);
+        }
+    }
+    if (live) tpe_store_scalars(p, env, v);
+    __syncthreads();
+    if (p.obs) tpe_copy_out(p, p.obs, img, env0, false);
+}
+
+}  // namespace lbk

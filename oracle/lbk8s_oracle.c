@@ -98,7 +98,7 @@ static void philox4x32_10(uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t ou
 }
 
 /* domains of the framework's draw map */
-enum { D_INIT = 1, D_NODE = 2, D_EP = 3, D_TOPO = 4, D_REQ_X = 5, D_REQ_I = 6, D_ACT = 7, D_REQ_X2 = 8 };
+enum { D_INIT = 1, D_NODE = 2, D_EP = 3, D_TOPO = 4, D_REQ_X = 5, D_REQ_I = 6, D_ACT = 7 };
 
 static void draw(const orc_env* s, int64_t b, uint32_t episode, uint32_t slot, uint32_t dom,
                  uint32_t out[4]) {
@@ -303,12 +303,11 @@ static void reset_one(orc_env* s, int64_t b, const orc_reset_trace* tr) {
     int r, n;
     if (tr) { x1 = tr->x1[b]; x2 = tr->x2[b]; r = tr->r[b]; n = tr->n[b]; }
     else {
-        uint32_t wi[4], w2[4];
+        uint32_t wi[4];
         draw(s, b, ep, 0, D_REQ_X, w);
-        draw(s, b, ep, 0, D_REQ_X2, w2);
         draw(s, b, ep, 0, D_REQ_I, wi);
         x1 = (1.0 / s->c.arrival_rate) * std_exp(w[0], w[1]);
-        x2 = s->c.call_duration * std_exp(w2[0], w2[1]);
+        x2 = s->c.call_duration * std_exp(w[2], w[3]);
         r = (int)bounded(wi[0], 7); n = (int)bounded(wi[1], (uint32_t)N);
     }
     next_request(s, b, x1, x2, r, n);
@@ -440,12 +439,11 @@ void orc_step(void* h, const int32_t* actions, float* obs, float* reward, uint8_
         int r, n;
         if (st_tr) { x1 = st_tr->x1[b]; x2 = st_tr->x2[b]; r = st_tr->r[b]; n = st_tr->n[b]; }
         else {
-            uint32_t w[4], w2[4], wi[4];
+            uint32_t w[4], wi[4];
             draw(s, b, s->episode[b], (uint32_t)s->step[b], D_REQ_X, w);
-            draw(s, b, s->episode[b], (uint32_t)s->step[b], D_REQ_X2, w2);
             draw(s, b, s->episode[b], (uint32_t)s->step[b], D_REQ_I, wi);
             x1 = (1.0 / s->c.arrival_rate) * std_exp(w[0], w[1]);
-            x2 = s->c.call_duration * std_exp(w2[0], w2[1]);
+            x2 = s->c.call_duration * std_exp(w[2], w[3]);
             r = (int)bounded(wi[0], 7); n = (int)bounded(wi[1], (uint32_t)s->N);
         }
         next_request(s, b, x1, x2, r, n);
