@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Kernel micro-bench: lb_step time vs batch size and scenario (one process, HIP events).
+
+    python tools/kbench.py [--configs default,cfg1,e64_multi] [--sizes 16,18,20,22]
+Prints one JSON line per (config, B): ms per step, env-steps/s, algorithmic GB/s.
+"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "gym-loadbalancing_amd")]
+
+from bench import CONFIGS, algorithmic_bytes  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="default,cfg1,e64_multi")
+    ap.add_argument("--sizes", default="16,18,20,22")
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--ring", type=int, default=16)
+    args = ap.parse_args()
+    import torch
+
+    from lbk8s import LBVecEnv
+    dev = torch.device("cuda", 0)
+    for name in args.configs.split(","):
+        for lg in (int(x) for x in args.sizes.split(",")):
+            B = 1 << lg
+            if name == "e64_multi" and lg > 20:
+                continue
+            env = LBVecEnv(B, device=dev, seed=0, as_tensors=True, **CONFIGS[name])
+            R = env.cfg.obs_rows
+            T = args.ring
+            ring = torch.empty((T, B, R, 8), dtype=torch.float32, device=dev)
+            rew = torch.empty((T, B), dtype=torch.float32, device=dev)
+            dn = torch.empty((T, B), dtype=torch.uint8, device=dev)
+            acts = torch.randint(0, env.action_space.n, (16, B), dtype=torch.int32, device=dev)
+            env.reset()
+            for i in range(20):
+                env.step_device(acts[i % 16], obs_out=ring[i % T], reward_out=rew[i % T], done_out=dn[i % T])
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            s.record()
+            for i in range(args.steps):
+                env.step_device(acts[i % 16], obs_out=ring[i % T], reward_out=rew[i % T], done_out=dn[i % T])
+            e.record()
+            torch.cuda.synchronize()
+            ms = s.elapsed_time(e) / args.steps
+            b = algorithmic_bytes(env.cfg)
+            print(json.dumps(dict(config=name, envs=B, ms_per_step=round(ms, 5),
+                                  env_steps_per_s=B / ms * 1e3, alg_GBps=b * B / ms / 1e6,
+                                  bytes_per_env_step=b)), flush=True)
+            del env, ring, rew, dn, acts
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
