@@ -39,6 +39,10 @@ __device__ __forceinline__ void tpe_request_draws(const Params& p, int64_t env, 
             x1 = p.tr.step_x1[env]; x2 = p.tr.step_x2[env]; r = p.tr.step_r[env]; n = p.tr.step_n[env];
         }
     } else {  // draw map: (D_REQ_X) -> x1 words 0,1 / x2 words 2,3; (D_REQ_I) -> r word 0 / n word 1
+#ifdef LB_ABL_NO_RNG
+        x1 = 0.01; x2 = 1.0; r = (int)(slot % 7); n = (int)(env % p.N);
+        return;
+#endif
         U4 a = draw(p, env, episode, slot, D_REQ_X);
         U4 b = draw(p, env, episode, slot, D_REQ_I);
         x1 = p.inv_rate * std_exp(a.x, a.y);
@@ -88,7 +92,13 @@ __device__ __forceinline__ void tpe_copy_out(const Params& p, float* out, const 
         } else {
             v = half == 0 ? make_float4(-1.f, -1.f, -1.f, -1.f) : make_float4(-1.f, (float)rz, thr, dt);
         }
+#ifdef LB_ABL_NT
+        typedef float f4n __attribute__((ext_vector_type(4)));
+        f4n nv = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(nv, reinterpret_cast<f4n*>(out + (env0 + el) * (int64_t)p.R * 8) + piece);
+#else
         reinterpret_cast<float4*>(out + (env0 + el) * (int64_t)p.R * 8)[piece] = v;
+#endif
     }
 }
 
@@ -291,8 +301,13 @@ __global__ __launch_bounds__(BLOCK) void k_step_tpe(Params p) {
     for (int e = 0; e < TPE_E; ++e) {
         if (e < E) {
             const int j = ed_j(ed[e]);
+#ifdef LB_ABL_NO_LUT
+            const double l = lat0[e];
+            const double c = (double)em_c0(em[e]);
+#else
             const double l = p.lat_lut[(int)lat0[e] * JCAP + j];
             const double c = p.cpu_lut[em_c0(em[e]) * JCAP + ed_m(ed[e])];
+#endif
             float ol = j == 0 ? (float)lat0[e] : (float)l;
             float oc = (float)c;
             if (accept && e == ai) { ol = (float)next_lat; oc = (float)next_cpu; }
@@ -322,10 +337,20 @@ __global__ __launch_bounds__(BLOCK) void k_step_tpe(Params p) {
         // decrease in next_request() (:1137-1143) -> the history counters advance
         const uint32_t edA_new = ((oA == ai ? (uint32_t)Mn : (uint32_t)ed_M(edA)) << 20) |
                                  ((uint32_t)Mn << 10) | (uint32_t)jn;
+#ifdef LB_ABL_ED_FULL
+        const uint32_t edO_new = (edO & ~(0x3FFu << 20)) | ((uint32_t)Mn << 20);
+#pragma unroll
+        for (int e = 0; e < TPE_E; ++e)
+            if (e == oA) ed[e] = edO_new;
+#pragma unroll
+        for (int e = 0; e < TPE_E; ++e)
+            if (e == ai) ed[e] = edA_new;
+#else
         if (live) {
             if (oA != ai) p.edyn[(int64_t)oA * p.B + env] = (edO & ~(0x3FFu << 20)) | ((uint32_t)Mn << 20);
             p.edyn[(int64_t)ai * p.B + env] = edA_new;
         }
+#endif
         v.s.penalty = 0;
         reward = accept_reward(p, sel_lat, tl, sel_cpu, v.acc2, v.s.acc);
         v.last_r = reward;
@@ -371,8 +396,17 @@ __global__ __launch_bounds__(BLOCK) void k_step_tpe(Params p) {
         }
     }
     if (live) tpe_store_scalars(p, env, v);
+#ifdef LB_ABL_ED_FULL
+    if (live && !do_reset) {
+#pragma unroll
+        for (int e = 0; e < TPE_E; ++e)
+            if (e < E) p.edyn[(int64_t)e * p.B + env] = ed[e];
+    }
+#endif
     __syncthreads();
+#ifndef LB_ABL_NO_OBS
     if (p.obs) tpe_copy_out(p, p.obs, img, env0, false);
+#endif
 }
 
 }  // namespace lbk
