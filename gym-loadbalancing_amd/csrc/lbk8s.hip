@@ -29,23 +29,23 @@ namespace lbk {
 // same step); CPU[c][M]: node cpu after M selections (:861-887 then :937-960).
 __global__ void k_luts(double* lat_lut, double* cpu_lut) {
     int row = blockIdx.x * blockDim.x + threadIdx.x;
+    // column-major ([j][k]): envs stepping in lockstep hold similar counters, so one
+    // step's lookups touch a few columns (L1/L2-resident) rather than scattered rows
     if (row < LAT_ROWS) {
-        double* o = lat_lut + (int64_t)row * JCAP;
         double v = (double)row;
-        o[0] = v;
+        lat_lut[row] = v;
         for (int j = 1; j < JCAP; ++j) {
             double inc = clamp_lat(trunc(v) * 1.5);
             v = clamp_lat(trunc(inc) / 1.15);
-            o[j] = v;
+            lat_lut[(int64_t)j * LAT_ROWS + row] = v;
         }
     } else if (row < LAT_ROWS + CPU_ROWS) {
         int c = row - LAT_ROWS;
-        double* o = cpu_lut + (int64_t)c * JCAP;
         double w = (double)c;
-        o[0] = w;
+        cpu_lut[c] = w;
         for (int m = 1; m < JCAP; ++m) {
             w = clamp_cpu(clamp_cpu(w * 1.15) / 1.15);
-            o[m] = w;
+            cpu_lut[(int64_t)m * CPU_ROWS + c] = w;
         }
     }
 }

@@ -100,14 +100,14 @@ __device__ __forceinline__ void slice_write_obs(const Params& p, float* out, int
                                    (float)topo_val(v.topo, z, v.s.rz));
             float4 b = make_float4(v.olat[k], rz, thr, dt);
             float4* row = reinterpret_cast<float4*>(base + e * 8);
-            row[0] = a;
-            row[1] = b;
+            st_stream(row, a);
+            st_stream(row + 1, b);
         }
     }
     if (p.rejection && lane == (p.E % W)) {
         float4* row = reinterpret_cast<float4*>(base + p.E * 8);
-        row[0] = make_float4(-1.f, -1.f, -1.f, -1.f);
-        row[1] = make_float4(-1.f, rz, thr, dt);
+        st_stream(row, make_float4(-1.f, -1.f, -1.f, -1.f));
+        st_stream(row + 1, make_float4(-1.f, rz, thr, dt));
     }
 }
 
@@ -307,15 +307,15 @@ __global__ __launch_bounds__(BLOCK) void k_step_slice(Params p) {
     const int jn = jA < CMAX ? jA + 1 : CMAX;
     const int k0A = (int)lat0A, c0A = em_c0(emA);
     // selected endpoint before (selected_*) and after (inc+dec) this step's update
-    const double lut_selA = p.lat_lut[k0A * JCAP + jA];
-    const double sel_cpu = p.cpu_lut[c0A * JCAP + ed_m(edA)];
-    const double next_lat = p.lat_lut[k0A * JCAP + jn];
-    const double next_cpu = p.cpu_lut[c0A * JCAP + Mn];
+    const double lut_selA = p.lat_lut[(jA) * LAT_ROWS + k0A];
+    const double sel_cpu = p.cpu_lut[(ed_m(edA)) * CPU_ROWS + c0A];
+    const double next_lat = p.lat_lut[(jn) * LAT_ROWS + k0A];
+    const double next_cpu = p.cpu_lut[(Mn) * CPU_ROWS + c0A];
 #pragma unroll
     for (int k = 0; k < EPL; ++k) {  // observed values of every endpoint
-        const double l = p.lat_lut[(int)v.lat0[k] * JCAP + ed_j(v.ed[k])];
+        const double l = p.lat_lut[ed_j(v.ed[k]) * LAT_ROWS + (int)v.lat0[k]];
         v.olat[k] = (float)(ed_j(v.ed[k]) == 0 ? v.lat0[k] : l);
-        v.ocpu[k] = (float)p.cpu_lut[em_c0(v.em[k]) * JCAP + ed_m(v.ed[k])];
+        v.ocpu[k] = (float)p.cpu_lut[ed_m(v.ed[k]) * CPU_ROWS + em_c0(v.em[k])];
     }
 
     // ---- take_action (:578-686)

@@ -92,13 +92,7 @@ __device__ __forceinline__ void tpe_copy_out(const Params& p, float* out, const 
         } else {
             v = half == 0 ? make_float4(-1.f, -1.f, -1.f, -1.f) : make_float4(-1.f, (float)rz, thr, dt);
         }
-#ifdef LB_ABL_NT
-        typedef float f4n __attribute__((ext_vector_type(4)));
-        f4n nv = {v.x, v.y, v.z, v.w};
-        __builtin_nontemporal_store(nv, reinterpret_cast<f4n*>(out + (env0 + el) * (int64_t)p.R * 8) + piece);
-#else
-        reinterpret_cast<float4*>(out + (env0 + el) * (int64_t)p.R * 8)[piece] = v;
-#endif
+        st_stream(reinterpret_cast<float4*>(out + (env0 + el) * (int64_t)p.R * 8) + piece, v);
     }
 }
 
@@ -200,14 +194,14 @@ __device__ void tpe_reset(const Params& p, int64_t env, TEnv& v, uint32_t* me) {
 }
 
 __device__ __forceinline__ void tpe_store_scalars(const Params& p, int64_t env, const TEnv& v) {
-    p.t[env] = v.t;
-    p.sc[env] = sc_pack(v.s);
-    p.acc2[env] = v.acc2;
-    p.acc3[env] = v.acc3;
-    p.sum_lat[env] = v.sum_lat;
-    p.sum_cpu[env] = v.sum_cpu;
-    p.total[env] = v.total;
-    if (p.reward_fn != LB_REWARD_NAIVE) p.last_r[env] = v.last_r;
+    st_state(p.t + env, v.t);
+    st_state(p.sc + env, sc_pack(v.s));
+    st_state(p.acc2 + env, v.acc2);
+    st_state(p.acc3 + env, v.acc3);
+    st_state(p.sum_lat + env, v.sum_lat);
+    st_state(p.sum_cpu + env, v.sum_cpu);
+    st_state(p.total + env, v.total);
+    if (p.reward_fn != LB_REWARD_NAIVE) st_state(p.last_r + env, v.last_r);
 }
 
 template <bool TRACE>
@@ -253,23 +247,23 @@ __global__ __launch_bounds__(BLOCK) void k_step_tpe(Params p) {
 #pragma unroll
     for (int e = 0; e < TPE_E; ++e) {
         const int64_t i = (int64_t)e * p.B + ev;
-        lat0[e] = e < E ? p.lat0[i] : 0.0;
-        em[e] = e < E ? p.emeta[i] : 0u;
-        ed[e] = e < E ? p.edyn[i] : 0u;
+        lat0[e] = e < E ? ld_state(p.lat0 + i) : 0.0;
+        em[e] = e < E ? ld_state(p.emeta + i) : 0u;
+        ed[e] = e < E ? ld_state(p.edyn + i) : 0u;
     }
-    const int a = p.actions[ev];
-    v.t = p.t[ev];
-    v.s = sc_unpack(p.sc[ev]);
-    v.topo = p.topo[ev];
-    v.zcap = p.zcap[ev];
-    v.nz0 = p.nzone[ev];
-    v.nz1 = p.NZW > 1 ? p.nzone[p.B + ev] : 0;
-    v.acc2 = p.acc2[ev];
-    v.acc3 = p.acc3[ev];
-    v.sum_lat = p.sum_lat[ev];
-    v.sum_cpu = p.sum_cpu[ev];
-    v.total = p.total[ev];
-    v.last_r = p.reward_fn != LB_REWARD_NAIVE ? p.last_r[ev] : 0.0;
+    const int a = ld_state(p.actions + ev);
+    v.t = ld_state(p.t + ev);
+    v.s = sc_unpack(ld_state(p.sc + ev));
+    v.topo = ld_state(p.topo + ev);
+    v.zcap = ld_state(p.zcap + ev);
+    v.nz0 = ld_state(p.nzone + ev);
+    v.nz1 = p.NZW > 1 ? ld_state(p.nzone + p.B + ev) : 0;
+    v.acc2 = ld_state(p.acc2 + ev);
+    v.acc3 = ld_state(p.acc3 + ev);
+    v.sum_lat = ld_state(p.sum_lat + ev);
+    v.sum_cpu = ld_state(p.sum_cpu + ev);
+    v.total = ld_state(p.total + ev);
+    v.last_r = p.reward_fn != LB_REWARD_NAIVE ? ld_state(p.last_r + ev) : 0.0;
 
     // ---- phase 1: decode the action, pick the selected endpoint, table lookups
     v.s.step = v.s.step < 0xFFFF ? v.s.step + 1 : 0xFFFF;
@@ -292,10 +286,10 @@ __global__ __launch_bounds__(BLOCK) void k_step_tpe(Params p) {
     const int Mn = ed_M(edO) < CMAX ? ed_M(edO) + 1 : CMAX;
     const int jn = jA < CMAX ? jA + 1 : CMAX;
     const int k0A = (int)lat0A, c0A = em_c0(emA);
-    const double lut_selA = p.lat_lut[k0A * JCAP + jA];
-    const double sel_cpu = p.cpu_lut[c0A * JCAP + ed_m(edA)];
-    const double next_lat = p.lat_lut[k0A * JCAP + jn];
-    const double next_cpu = p.cpu_lut[c0A * JCAP + Mn];
+    const double lut_selA = p.lat_lut[(jA) * LAT_ROWS + k0A];
+    const double sel_cpu = p.cpu_lut[(ed_m(edA)) * CPU_ROWS + c0A];
+    const double next_lat = p.lat_lut[(jn) * LAT_ROWS + k0A];
+    const double next_cpu = p.cpu_lut[(Mn) * CPU_ROWS + c0A];
     int cnt = 0;  // #{e != ai : loads[e] <= loads[ai]} for the O(E) Gini update
 #pragma unroll
     for (int e = 0; e < TPE_E; ++e) {
@@ -305,8 +299,8 @@ __global__ __launch_bounds__(BLOCK) void k_step_tpe(Params p) {
             const double l = lat0[e];
             const double c = (double)em_c0(em[e]);
 #else
-            const double l = p.lat_lut[(int)lat0[e] * JCAP + j];
-            const double c = p.cpu_lut[em_c0(em[e]) * JCAP + ed_m(ed[e])];
+            const double l = p.lat_lut[(j) * LAT_ROWS + (int)lat0[e]];
+            const double c = p.cpu_lut[ed_m(ed[e]) * CPU_ROWS + em_c0(em[e])];
 #endif
             float ol = j == 0 ? (float)lat0[e] : (float)l;
             float oc = (float)c;
@@ -347,8 +341,8 @@ __global__ __launch_bounds__(BLOCK) void k_step_tpe(Params p) {
             if (e == ai) ed[e] = edA_new;
 #else
         if (live) {
-            if (oA != ai) p.edyn[(int64_t)oA * p.B + env] = (edO & ~(0x3FFu << 20)) | ((uint32_t)Mn << 20);
-            p.edyn[(int64_t)ai * p.B + env] = edA_new;
+            if (oA != ai) st_state(p.edyn + (int64_t)oA * p.B + env, (edO & ~(0x3FFu << 20)) | ((uint32_t)Mn << 20));
+            st_state(p.edyn + (int64_t)ai * p.B + env, edA_new);
         }
 #endif
         v.s.penalty = 0;
@@ -378,7 +372,7 @@ __global__ __launch_bounds__(BLOCK) void k_step_tpe(Params p) {
     }
     const bool done = live && v.s.step == p.L;  // (:472)
     if (live) {
-        if (p.reward) p.reward[env] = (float)reward;
+        if (p.reward) st_state(p.reward + env, (float)reward);
         if (p.done) p.done[env] = (uint8_t)done;
     }
     tpe_image_env(me, v, done ? TPE_FLAG : 0);
@@ -400,7 +394,7 @@ __global__ __launch_bounds__(BLOCK) void k_step_tpe(Params p) {
     if (live && !do_reset) {
 #pragma unroll
         for (int e = 0; e < TPE_E; ++e)
-            if (e < E) p.edyn[(int64_t)e * p.B + env] = ed[e];
+            if (e < E) st_state(p.edyn + (int64_t)e * p.B + env, ed[e]);
     }
 #endif
     __syncthreads();

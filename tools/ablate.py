@@ -27,7 +27,7 @@ def load(path):
 
 
 def main():
-    names = sys.argv[1].split(",") if len(sys.argv) > 1 else ["base", "NO_LUT", "NO_OBS", "NO_RNG", "ED_FULL", "NT"]
+    names = sys.argv[1].split(",") if len(sys.argv) > 1 else ["base", "PLAIN_OBS", "NO_LUT", "NO_OBS", "NO_RNG", "ED_FULL", "NT_STATE", "NT_LOAD"]
     B = 1 << 20
     dev = torch.device("cuda", 0)
     cfg = LBConfig()
