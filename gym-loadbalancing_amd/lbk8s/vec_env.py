@@ -71,7 +71,7 @@ class LazyInfos:
             return self._cache[i]
         self._host()
         env = self._env
-        if self._d[i]:
+        if self._d[i] and env.auto_reset:  # ep_stats rows are written by the auto-reset
             st = env._host_ep_stats()[i]
         else:
             if self._stats is None:

@@ -1,0 +1,148 @@
+"""GPU tests of the drop-in surfaces and full-size properties (through the C ABI).
+
+* single-env LoadBalancerK8sEnv + host greedy policies == C oracle (run_baselines loop);
+* LBVecEnv SB3 surface: infos (13 keys, terminal_observation, VecMonitor episode),
+  env_method / get_attr / step_async / as_tensors;
+* T4 sharding invariance on the device (1 shard == 2 shards with env id offsets);
+* 2^20-env properties: value ranges, done cadence, episode-statistics invariants,
+  determinism, status word.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_single_env_greedy_matches_oracle(oracle_mod, tmp_path):
+    from lbk8s import LoadBalancerK8sEnv
+    from lbk8s.baselines import POLICIES
+    cfg = dict(num_endpoints=6, num_nodes=48, num_zones=12, reward_function="naive",
+               latency_weight=1.0, cpu_weight=0.0, gini_weight=0.0, episode_length=30)
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        for kind, pol in POLICIES.items():
+            env = LoadBalancerK8sEnv(seed=42, file_results_name=f"res_{kind}", **cfg)
+            orc = oracle_mod.OracleBatch(cfg, 1, trace=False, auto_reset=False, seed=42)
+            orc.init()
+            for ep in range(3):
+                obs = env.reset()
+                np.testing.assert_array_equal(obs, orc.reset()[0])
+                done, ret = False, 0.0
+                while not done:
+                    a = pol(env, env.action_masks())
+                    assert a == int(orc.policy_greedy(kind)[0])
+                    obs, r, done, info = env.step(a)
+                    o2, r2, d2, _, _ = orc.step(np.array([a], np.int32))
+                    np.testing.assert_array_equal(obs, o2[0])
+                    assert r == r2[0] and done == d2[0]
+                    ret += r
+                assert ret == cfg["episode_length"]  # greedy never rejects (masks all True)
+                assert info["ep_accepted_requests"] == cfg["episode_length"]
+            rows = open(f"res_{kind}.csv").read().strip().splitlines()
+            assert len(rows) == 3 and rows[0].startswith("1,")
+            assert len(open("no_cost_updated.csv").read().strip().splitlines()) >= 3
+    finally:
+        os.chdir(cwd)
+
+
+def test_vecenv_sb3_surface():
+    from lbk8s import INFO_KEYS, LBVecEnv
+    B = 16
+    env = LBVecEnv(B, seed=1, monitor=True, info_keywords=("gini", "avg_cost"), episode_length=5,
+                   reward_function="multi")
+    assert env.num_envs == B and env.observation_space.shape == (9, 8) and env.action_space.n == 9
+    masks = np.array(env.env_method("action_masks"))
+    assert masks.shape == (B, 9) and masks.all()
+    with pytest.raises(TypeError):
+        env.step(np.zeros(B, np.int32))  # before reset: reference raises TypeError
+    obs = env.reset()
+    assert obs.shape == (B, 9, 8) and obs.dtype == np.float32
+    for s in range(5):
+        env.step_async(np.full(B, s % 9, np.int32))
+        obs, rew, done, infos = env.step_wait()
+        assert len(infos) == B
+        info = infos[3]
+        for k in INFO_KEYS:
+            assert k in info
+        if s < 4:
+            assert not done.any() and "episode" not in info
+    assert done.all()
+    for i, info in enumerate(infos):
+        assert info["terminal_observation"].shape == (9, 8)
+        ep = info["episode"]
+        assert ep["l"] == 5 and "gini" in ep and "avg_cost" in ep
+        assert abs(ep["r"] - float(np.float32(ep["r"]))) < 1e-3
+    # the post-reset obs differs from the terminal one (new scenario)
+    assert not np.array_equal(obs[0], infos[0]["terminal_observation"])
+    topo = env.get_attr("endpoint_topology_latency")
+    assert len(topo) == B and topo[0].shape == (8,)
+    assert env.get_attr("num_endpoints", indices=[0, 1]) == [8, 8]
+    tenv = LBVecEnv(B, seed=1, as_tensors=True)
+    o = tenv.reset()
+    assert isinstance(o, torch.Tensor) and o.is_cuda
+    o, r, d, _ = tenv.step(torch.zeros(B, dtype=torch.int64, device="cuda"))
+    assert r.is_cuda and d.dtype == torch.bool
+
+
+def test_sharding_invariance_device():
+    from lbk8s import LBVecEnv
+    B = 4096
+    cfg = dict(num_endpoints=8, reward_function="fairness")
+    full = LBVecEnv(B, seed=11, as_tensors=True, **cfg)
+    parts = [LBVecEnv(B // 2, seed=11, env_id_offset=o, as_tensors=True, **cfg) for o in (0, B // 2)]
+    a0 = full.reset().clone()
+    torch.testing.assert_close(a0, torch.cat([p.reset().clone() for p in parts]), rtol=0, atol=0)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(0)
+    for s in range(150):
+        a = torch.randint(0, 9, (B,), dtype=torch.int32, device="cuda", generator=gen)
+        o1, r1, _, _ = full.step(a)
+        outs = [p.step(a[i * (B // 2):(i + 1) * (B // 2)]) for i, p in enumerate(parts)]
+        assert torch.equal(o1, torch.cat([x[0] for x in outs]))
+        assert torch.equal(r1, torch.cat([x[1] for x in outs]))
+
+
+def test_full_size_properties():
+    from lbk8s import LBVecEnv
+    from lbk8s.info import ST_ACC, ST_GINI, ST_INTER, ST_INTRA, ST_LENGTH, ST_RETURN
+    B = 1 << 20
+    env = LBVecEnv(B, seed=2024, as_tensors=True)
+    obs = env.reset()
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(1)
+    thresholds = torch.tensor([150., 200., 250., 375., 400., 450., 500.], device="cuda")
+    for s in range(1, 201):
+        a = torch.randint(0, 9, (B,), dtype=torch.int32, device="cuda", generator=gen)
+        obs, rew, done, _ = env.step(a)
+        if s % 50 == 0 or s % 100 == 0:
+            ep = obs[:, :8]
+            assert ep[..., 0].min() >= 0 and ep[..., 0].max() <= 3
+            assert ep[..., 1].min() >= 2 and ep[..., 1].max() <= 8 * 24
+            assert ep[..., 2].min() >= 1 and ep[..., 2].max() <= 100
+            assert ep[..., 3].min() >= 1 and ep[..., 3].max() <= 499
+            assert ep[..., 4].min() >= 1 and ep[..., 4].max() <= 500
+            assert torch.isin(obs[:, 0, 6], thresholds).all()
+            assert (obs[:, :, 7] > 0).all() and (obs[:, 8, :5] == -1).all()
+            assert ((rew == 1) | (rew == -1)).all()
+        assert bool(done.all()) == (s % 100 == 0) and bool(done.any()) == (s % 100 == 0)
+        if s % 100 == 0:
+            st = env.ep_stats
+            assert (st[:, ST_LENGTH] == 100).all()
+            assert (st[:, ST_INTRA] + st[:, ST_INTER] == st[:, ST_ACC]).all()
+            assert torch.allclose(st[:, ST_RETURN], 2 * st[:, ST_ACC] - 100)  # naive: +1 / -1
+            assert (st[:, ST_GINI] >= 0).all() and (st[:, ST_GINI] < 1).all()
+            frac = (st[:, ST_ACC] / 100).mean().item()
+            assert abs(frac - 8 / 9) < 0.002  # uniform random actions accept 8 of 9
+    assert env.status() == 0
+    # determinism: an identically seeded env reproduces the stream
+    env2 = LBVecEnv(B, seed=2024, as_tensors=True)
+    env2.reset()
+    gen.manual_seed(1)
+    for s in range(1, 201):
+        a = torch.randint(0, 9, (B,), dtype=torch.int32, device="cuda", generator=gen)
+        o2, _, _, _ = env2.step(a)
+    assert torch.equal(o2, obs)
