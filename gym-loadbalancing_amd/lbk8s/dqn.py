@@ -1,0 +1,163 @@
+"""GPU-resident deep-sets DQN.
+
+Restates envs/dqn_deepset.py:44-231 on device tensors: epsilon-greedy with ONE
+random.random() deciding exploration for all envs (:127), masked argmax of Q (:134-142),
+an SB3-style replay buffer resident in HBM (buffer_size // num_envs slots of num_envs
+transitions, uniform (slot, env) sampling; next_obs stored as returned — the reset obs
+for finished envs, as the reference stores it, :158-174), TD target from the target
+network's max (:180-186), MSE loss, Adam, hard target copy every
+target_network_frequency steps (tau = 1, :199-203).  total_timesteps counts VECTOR steps
+(:122).
+
+Multi-GPU: gradients averaged with one all_reduce per train step (RCCL); every rank keeps
+its own envs and replay.
+"""
+import random
+import time
+from copy import deepcopy
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from torch import optim
+
+from .deepsets import DQNDeepSetAgent, HUGE_NEG, allreduce_gradients
+
+
+def linear_schedule(start_e: float, end_e: float, duration: float, t: int) -> float:
+    slope = (end_e - start_e) / duration
+    return max(slope * t + start_e, end_e)
+
+
+class DeviceReplayBuffer:
+    """SB3 ReplayBuffer semantics (n_envs-major circular storage) with device tensors."""
+
+    def __init__(self, buffer_size, num_envs, obs_shape, device, generator):
+        self.n_envs = num_envs
+        self.size = max(buffer_size // num_envs, 1)
+        self.obs = torch.zeros((self.size, num_envs) + tuple(obs_shape), device=device)
+        self.next_obs = torch.zeros_like(self.obs)
+        self.actions = torch.zeros((self.size, num_envs), dtype=torch.long, device=device)
+        self.rewards = torch.zeros((self.size, num_envs), device=device)
+        self.dones = torch.zeros((self.size, num_envs), device=device)
+        self.pos, self.full = 0, False
+        self.gen = generator
+
+    def add(self, obs, next_obs, actions, rewards, dones):
+        p = self.pos
+        self.obs[p].copy_(obs)
+        self.next_obs[p].copy_(next_obs)
+        self.actions[p].copy_(actions)
+        self.rewards[p].copy_(rewards)
+        self.dones[p].copy_(dones)
+        self.pos += 1
+        if self.pos == self.size:
+            self.full, self.pos = True, 0
+
+    def sample(self, batch_size):
+        upper = self.size if self.full else self.pos
+        dev = self.obs.device
+        bi = torch.randint(0, upper, (batch_size,), device=dev, generator=self.gen)
+        ei = torch.randint(0, self.n_envs, (batch_size,), device=dev, generator=self.gen)
+        return (self.obs[bi, ei], self.actions[bi, ei][:, None], self.next_obs[bi, ei],
+                self.dones[bi, ei][:, None], self.rewards[bi, ei][:, None])
+
+
+def dqn_loss(q_network, target_network, obs, actions, next_obs, rewards, dones, gamma):
+    """dqn_deepset.py:180-187 -> (loss, td_target, old_val)."""
+    with torch.no_grad():
+        target_max, _ = target_network(next_obs).max(dim=1)
+        td_target = rewards.flatten() + gamma * target_max * (1 - dones.flatten())
+    old_val = q_network(obs).gather(1, actions).squeeze()
+    return F.mse_loss(td_target, old_val), td_target, old_val
+
+
+class DQN_DeepSets:
+    def __init__(self, env, seed=1, torch_deterministic=True, num_steps: int = 100, learning_rate=2.5e-4,
+                 buffer_size=10000, gamma=0.99, tau=1.0, n_minibatches: int = 4, target_network_frequency=500,
+                 batch_size=128, start_e=1, end_e=0.05, exploration_fraction=0.5, learning_starts=10000,
+                 train_frequency=10, device=None, log_fn=None):
+        self.env = env
+        self.device = torch.device(device) if device is not None else env.device
+        self.num_envs = env.num_envs
+        self.num_steps, self.seed, self.learning_rate = num_steps, seed, learning_rate
+        self.buffer_size, self.gamma, self.tau = buffer_size, gamma, tau
+        self.target_network_frequency, self.batch_size = target_network_frequency, batch_size
+        self.start_e, self.end_e, self.exploration_fraction = start_e, end_e, exploration_fraction
+        self.learning_starts, self.train_frequency = learning_starts, train_frequency
+        self.log_fn = log_fn or (lambda d: None)
+        random.seed(seed)
+        np.random.seed(seed)
+        torch.manual_seed(seed)
+        if torch_deterministic:
+            torch.backends.cudnn.deterministic = True
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed)
+        self.q_network = DQNDeepSetAgent(env).to(self.device)
+        self.target_network = deepcopy(self.q_network)
+        self.optimizer = optim.Adam(self.q_network.parameters(), lr=learning_rate)
+        self.rb = DeviceReplayBuffer(buffer_size, self.num_envs, env.observation_space.shape, self.device, self.gen)
+        self._act = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
+        self._done_u8 = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
+        self._rew = torch.zeros(self.num_envs, device=self.device)
+        self._next_obs = torch.zeros((self.num_envs,) + tuple(env.observation_space.shape), device=self.device)
+        self.episode_returns = []
+        self.train_steps = 0
+
+    def select_actions(self, obs, masks, epsilon):
+        if random.random() < epsilon:  # one draw decides exploration for every env (:127)
+            probs = masks.float()
+            return torch.multinomial(probs, 1, generator=self.gen).squeeze(-1)
+        with torch.no_grad():
+            q = torch.where(masks, self.q_network(obs), torch.full((), HUGE_NEG, device=obs.device))
+        return torch.argmax(q, dim=1)
+
+    def train_step(self, global_step):
+        obs, actions, next_obs, dones, rewards = self.rb.sample(self.batch_size)
+        loss, _, old_val = dqn_loss(self.q_network, self.target_network, obs, actions, next_obs, rewards, dones,
+                                    self.gamma)
+        self.optimizer.zero_grad()
+        loss.backward()
+        allreduce_gradients(self.q_network)
+        self.optimizer.step()
+        self.train_steps += 1
+        if global_step % self.target_network_frequency == 0:
+            for tp, qp in zip(self.target_network.parameters(), self.q_network.parameters()):
+                tp.data.copy_(self.tau * qp.data + (1.0 - self.tau) * tp.data)
+        return loss
+
+    def learn(self, total_timesteps: int = 500000):
+        env = self.env
+        start = time.time()
+        env.reset()
+        obs = env.obs.clone()
+        masks = env.action_masks()
+        loss = None
+        for global_step in range(total_timesteps):
+            eps = linear_schedule(self.start_e, self.end_e, self.exploration_fraction * total_timesteps, global_step)
+            actions = self.select_actions(obs, masks, eps)
+            self._act.copy_(actions)
+            env.step_device(self._act, obs_out=self._next_obs, reward_out=self._rew, done_out=self._done_u8)
+            dones = self._done_u8.float()
+            if global_step % 100 == 0 and bool(self._done_u8.any()):
+                self.episode_returns.append(env.ep_stats[self._done_u8.bool(), 0].mean().item())
+            self.rb.add(obs, self._next_obs, actions, self._rew, dones)
+            obs.copy_(self._next_obs)
+            if global_step > self.learning_starts and global_step % self.train_frequency == 0:
+                loss = self.train_step(global_step)
+            if global_step % 1000 == 0:
+                self.log_fn(dict(global_step=global_step, epsilon=eps, sps=(global_step + 1) / (time.time() - start),
+                                 loss=None if loss is None else loss.item()))
+        return self
+
+    def predict(self, obs, masks=None):
+        with torch.no_grad():
+            x = torch.as_tensor(obs, dtype=torch.float32, device=self.device)
+            m = None if masks is None else torch.as_tensor(masks, dtype=torch.bool, device=self.device)
+            return self.q_network.get_action(x, m, deterministic=True)
+
+    def save(self, path):
+        torch.save(self.q_network.state_dict(), path)
+
+    def load(self, path):
+        self.q_network.load_state_dict(torch.load(path, map_location=self.device, weights_only=True))

@@ -1,0 +1,186 @@
+"""GPU-resident PPO for the deep-sets agent.
+
+Restates envs/ppo_deepset.py (CleanRL PPO, :53-300) on device tensors end to end:
+rollout storage (T, B, ...) filled by LBVecEnv.step_device (obs written straight into
+the storage slot, no host copies), GAE (:192-205), flattened minibatches, clipped policy
+and value losses, entropy bonus, advantage normalisation per minibatch, clip_grad_norm,
+Adam(eps=1e-5) (:216-267).  Hyper-parameter names and defaults are the reference's.
+Reference quirk kept: actions are sampled WITHOUT masks during the rollout (:169; the
+masks are all True anyway, :808-821) and the stored masks are used in the update.
+
+Multi-GPU: one process per GPU, each with its own envs (LBVecEnv env_id_offset); the
+gradients are averaged with one all_reduce per optimizer step (RCCL over xGMI).
+"""
+import time
+from typing import Optional
+
+import torch
+from torch import nn, optim
+
+from .deepsets import DeepSetAgent, allreduce_gradients
+
+
+def ppo_loss(agent, obs, actions, logprobs_old, masks, advantages, returns, values_old,
+             clip_coef=0.2, ent_coef=0.01, vf_coef=0.5, norm_adv=True, clip_vloss=True):
+    """One minibatch of ppo_deepset.py:227-263 -> (loss, pg_loss, v_loss, entropy, approx_kl, clipfrac)."""
+    # the same Categorical ops as the reference: the actor's last Gamma term shifts every
+    # logit of a set equally, so its true gradient is 0 and what autograd returns is
+    # rounding noise that only an identical op sequence reproduces
+    _, newlogprob, entropy, newvalue = agent.get_action_and_value(obs, actions.long(), masks)
+    newvalue = newvalue.view(-1)
+    logratio = newlogprob - logprobs_old
+    ratio = logratio.exp()
+    adv = advantages
+    if norm_adv:
+        adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+    pg_loss = torch.max(-adv * ratio, -adv * torch.clamp(ratio, 1 - clip_coef, 1 + clip_coef)).mean()
+    if clip_vloss:
+        v_unclipped = (newvalue - returns) ** 2
+        v_clipped = values_old + torch.clamp(newvalue - values_old, -clip_coef, clip_coef)
+        v_loss = 0.5 * torch.max(v_unclipped, (v_clipped - returns) ** 2).mean()
+    else:
+        v_loss = 0.5 * ((newvalue - returns) ** 2).mean()
+    entropy_loss = entropy.mean()
+    loss = pg_loss - ent_coef * entropy_loss + v_loss * vf_coef
+    with torch.no_grad():
+        approx_kl = ((ratio - 1) - logratio).mean()
+        clipfrac = ((ratio - 1.0).abs() > clip_coef).float().mean()
+    return loss, pg_loss, v_loss, entropy_loss, approx_kl, clipfrac
+
+
+def compute_gae(rewards, values, dones, next_value, next_done, gamma, gae_lambda):
+    """ppo_deepset.py:192-205 on (T, B) device tensors."""
+    T = rewards.shape[0]
+    advantages = torch.zeros_like(rewards)
+    lastgaelam = torch.zeros_like(rewards[0])
+    for t in reversed(range(T)):
+        if t == T - 1:
+            nextnonterminal = 1.0 - next_done
+            nextvalues = next_value
+        else:
+            nextnonterminal = 1.0 - dones[t + 1]
+            nextvalues = values[t + 1]
+        delta = rewards[t] + gamma * nextvalues * nextnonterminal - values[t]
+        lastgaelam = delta + gamma * gae_lambda * nextnonterminal * lastgaelam
+        advantages[t] = lastgaelam
+    return advantages, advantages + values
+
+
+class PPO_DeepSets:
+    def __init__(self, env, learning_rate: float = 2.5e-4, anneal_lr: bool = False, num_steps: int = 128,
+                 gae: bool = True, gae_lambda: float = 0.97, gamma: float = 0.95, n_minibatches: int = 4,
+                 update_epochs: int = 4, norm_adv: bool = True, clip_coef: float = 0.2,
+                 clip_vloss: bool = True, ent_coef: float = 0.01, vf_coef: float = 0.5,
+                 max_grad_norm: float = 0.5, target_kl: Optional[float] = None, seed: int = 1,
+                 device=None, log_fn=None):
+        self.env = env
+        self.device = torch.device(device) if device is not None else env.device
+        self.num_envs = env.num_envs
+        self.learning_rate, self.anneal_lr, self.num_steps = learning_rate, anneal_lr, num_steps
+        self.gae, self.gae_lambda, self.gamma = gae, gae_lambda, gamma
+        self.n_minibatches, self.update_epochs, self.norm_adv = n_minibatches, update_epochs, norm_adv
+        self.clip_coef, self.clip_vloss, self.ent_coef, self.vf_coef = clip_coef, clip_vloss, ent_coef, vf_coef
+        self.max_grad_norm, self.target_kl, self.seed = max_grad_norm, target_kl, seed
+        self.batch_size = int(self.num_envs * num_steps)
+        self.minibatch_size = int(self.batch_size // n_minibatches)
+        self.log_fn = log_fn or (lambda d: None)
+        torch.manual_seed(seed)
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed)
+        self.agent = DeepSetAgent(env).to(self.device)
+        self.optimizer = optim.Adam(self.agent.parameters(), lr=learning_rate, eps=1e-5)
+        T, B = num_steps, self.num_envs
+        R, A = env.observation_space.shape[0], env.action_space.n
+        dev = self.device
+        self.obs = torch.zeros((T, B, R, 8), device=dev)
+        self.actions = torch.zeros((T, B), device=dev)
+        self.masks = torch.ones((T, B, A), dtype=torch.bool, device=dev)
+        self.logprobs = torch.zeros((T, B), device=dev)
+        self.rewards = torch.zeros((T, B), device=dev)
+        self.dones = torch.zeros((T, B), device=dev)
+        self.values = torch.zeros((T, B), device=dev)
+        self._act = torch.zeros(B, dtype=torch.int32, device=dev)
+        self._done_u8 = torch.zeros(B, dtype=torch.uint8, device=dev)
+        self.episode_returns = []
+
+    def rollout(self, next_obs, next_done):
+        """Fill the (T, B) storage; returns the obs/done that follow the last step."""
+        env = self.env
+        for step in range(self.num_steps):
+            self.obs[step].copy_(next_obs)
+            self.dones[step] = next_done
+            action, logprob, value = self.agent.act(next_obs, generator=self.gen)  # no masks (:169)
+            self.values[step] = value
+            self.actions[step] = action.float()
+            self.logprobs[step] = logprob
+            self._act.copy_(action)
+            env.step_device(self._act, obs_out=env.obs, reward_out=self.rewards[step], done_out=self._done_u8)
+            next_obs = env.obs
+            next_done = self._done_u8.float()
+            if bool(self._done_u8.any()):
+                d = self._done_u8.bool()
+                self.episode_returns.append(env.ep_stats[d, 0].mean().item())
+        return next_obs, next_done
+
+    def update(self, next_obs, next_done):
+        with torch.no_grad():
+            next_value = self.agent.get_value(next_obs).reshape(1, -1)
+            advantages, returns = compute_gae(self.rewards, self.values, self.dones, next_value, next_done,
+                                              self.gamma, self.gae_lambda)
+        R = self.obs.shape[2]
+        b_obs = self.obs.reshape(-1, R, 8)
+        b_logprobs = self.logprobs.reshape(-1)
+        b_actions = self.actions.reshape(-1)
+        b_masks = self.masks.reshape(-1, self.masks.shape[-1])
+        b_adv, b_ret, b_val = advantages.reshape(-1), returns.reshape(-1), self.values.reshape(-1)
+        stats = {}
+        for epoch in range(self.update_epochs):
+            b_inds = torch.randperm(self.batch_size, device=self.device, generator=self.gen)
+            for start in range(0, self.batch_size, self.minibatch_size):
+                mb = b_inds[start:start + self.minibatch_size]
+                loss, pg, vl, ent, kl, cf = ppo_loss(
+                    self.agent, b_obs[mb], b_actions[mb], b_logprobs[mb], b_masks[mb], b_adv[mb], b_ret[mb],
+                    b_val[mb], self.clip_coef, self.ent_coef, self.vf_coef, self.norm_adv, self.clip_vloss)
+                self.optimizer.zero_grad()
+                loss.backward()
+                allreduce_gradients(self.agent)
+                nn.utils.clip_grad_norm_(self.agent.parameters(), self.max_grad_norm)
+                self.optimizer.step()
+            if self.target_kl is not None and kl > self.target_kl:
+                break
+        stats.update(loss=loss.item(), pg_loss=pg.item(), v_loss=vl.item(), entropy=ent.item(),
+                     approx_kl=kl.item(), clipfrac=cf.item())
+        return stats
+
+    def learn(self, total_timesteps: int = 500000):
+        env = self.env
+        start = time.time()
+        next_obs = env.reset()
+        if not isinstance(next_obs, torch.Tensor):
+            next_obs = env.obs
+        next_done = torch.zeros(self.num_envs, device=self.device)
+        num_updates = total_timesteps // self.batch_size
+        global_step = 0
+        for update in range(1, num_updates + 1):
+            if self.anneal_lr:
+                self.optimizer.param_groups[0]["lr"] = (1.0 - (update - 1.0) / num_updates) * self.learning_rate
+            next_obs, next_done = self.rollout(next_obs, next_done)
+            global_step += self.batch_size
+            stats = self.update(next_obs, next_done)
+            stats.update(update=update, global_step=global_step,
+                         sps=global_step / (time.time() - start),
+                         ep_return=self.episode_returns[-1] if self.episode_returns else float("nan"))
+            self.log_fn(stats)
+        return self
+
+    def predict(self, obs, masks=None):
+        with torch.no_grad():
+            x = torch.as_tensor(obs, dtype=torch.float32, device=self.device)
+            m = None if masks is None else torch.as_tensor(masks, dtype=torch.bool, device=self.device)
+            return self.agent.get_action(x, m, deterministic=True)
+
+    def save(self, path):
+        torch.save(self.agent.state_dict(), path)
+
+    def load(self, path):
+        self.agent.load_state_dict(torch.load(path, map_location=self.device, weights_only=True))

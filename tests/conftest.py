@@ -17,7 +17,9 @@ def pytest_configure(config):
 
 
 def golden_names(prefix=""):
-    return sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and f.startswith(prefix))
+    """Env-trajectory fixtures (the nn_* files hold network / learner goldens)."""
+    return sorted(f[:-4] for f in os.listdir(GOLDEN)
+                  if f.endswith(".npz") and f.startswith(prefix) and not f.startswith("nn_"))
 
 
 @pytest.fixture(scope="session")

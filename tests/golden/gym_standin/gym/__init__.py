@@ -10,7 +10,7 @@ product package or by the GPU tests.
 """
 import numpy as np
 
-from . import spaces, utils  # noqa: F401
+from . import spaces, utils, vector  # noqa: F401
 
 
 class Env:

@@ -1,0 +1,130 @@
+"""T6: deep-sets networks (A14), the PPO minibatch update (A16) and the DQN train step
+(A17) against fixtures produced by the reference's own modules (tests/golden/gen_golden_nn.py).
+
+Runs on the CPU here (torch CPU, same float32 ops as the reference: tolerance rtol 1e-5)
+and, marked gpu, on the MI355X (hipBLASLt float32 GEMMs: only the summation order
+differs; tolerance rtol 1e-4 / atol 1e-5 on activations, 1e-4 on parameters)."""
+import numpy as np
+import pytest
+import torch
+
+from nn_helpers import close, load_nn, state_dict_from
+
+DEVICES = ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
+
+
+def tol(device):
+    return dict(rtol=1e-5, atol=1e-6) if device == "cpu" else dict(rtol=1e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("name", ["e6", "e8", "e64"])
+def test_deepsets_forward_matches_reference(name, device):
+    from lbk8s.deepsets import DeepSetAgent, DQNDeepSetAgent
+    d = load_nn(f"nn_forward_{name}")
+    obs = torch.from_numpy(d["obs"]).to(device)
+    agent = DeepSetAgent(8).to(device)
+    agent.load_state_dict(state_dict_from(d, "agent__"))
+    q = DQNDeepSetAgent(8).to(device)
+    q.load_state_dict(state_dict_from(d, "qnet__"))
+    masks = torch.from_numpy(d["masks"]).to(device)
+    actions = torch.from_numpy(d["actions"]).to(device)
+    t = tol(device)
+    with torch.no_grad():
+        close(agent.actor(obs), d["logits"], what="logits", **t)
+        close(agent.critic(obs), d["value"], what="value", **t)
+        _, lp, ent, v = agent.get_action_and_value(obs, actions)
+        close(lp, d["logprob"], what="logprob", **t)
+        close(ent, d["entropy"], what="entropy", **t)
+        _, lpm, entm, _ = agent.get_action_and_value(obs, actions, masks)
+        close(lpm, d["logprob_masked"], what="logprob masked", **t)
+        close(entm, d["entropy_masked"], what="entropy masked", **t)
+        assert (agent.get_action(obs, masks).cpu().numpy() == d["mode_masked"]).all()
+        close(q(obs), d["q"], what="q", **t)
+        assert (q.get_action(obs, masks).cpu().numpy() == d["q_mode_masked"]).all()
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_ppo_minibatch_update_matches_reference(device):
+    from lbk8s.deepsets import DeepSetAgent
+    from lbk8s.ppo import ppo_loss
+    d = load_nn("nn_ppo_update")
+    agent = DeepSetAgent(8).to(device)
+    agent.load_state_dict(state_dict_from(d, "init__"))
+    f = lambda k, dt=torch.float32: torch.from_numpy(np.asarray(d[k])).to(device, dt)  # noqa: E731
+    loss, pg, vl, ent, kl, _ = ppo_loss(agent, f("obs"), f("actions"), f("logprobs"), f("masks", torch.bool),
+                                        f("advantages"), f("returns"), f("values"), clip_coef=0.2,
+                                        ent_coef=0.001, vf_coef=0.5)
+    t = tol(device)
+    for got, key in ((loss, "loss"), (pg, "pg_loss"), (vl, "v_loss"), (ent, "entropy_loss"), (kl, "approx_kl")):
+        close(got, d[key], what=key, **t)
+    opt = torch.optim.Adam(agent.parameters(), lr=2.5e-4, eps=1e-5)
+    opt.zero_grad()
+    loss.backward()
+    # gradients: elementwise, with an absolute floor of 1e-5 x the largest gradient (the
+    # actor's last Gamma has a true gradient of 0: its entries are rounding noise)
+    gmax = max(np.abs(d["grad__" + n.replace(".", "__")]).max() for n, _ in agent.named_parameters())
+    for n, p in agent.named_parameters():
+        close(p.grad, d["grad__" + n.replace(".", "__")], what="grad " + n, rtol=t["rtol"] * 10,
+              atol=max(t["atol"] * 10, 1e-5 * gmax))
+    gn = torch.nn.utils.clip_grad_norm_(agent.parameters(), 0.5)
+    close(gn, d["grad_norm"], what="grad norm", **t)
+    opt.step()
+    for n, p in agent.state_dict().items():
+        close(p, d["after__" + n.replace(".", "__")], what="param " + n, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_dqn_train_step_matches_reference(device):
+    from lbk8s.deepsets import DQNDeepSetAgent
+    from lbk8s.dqn import dqn_loss
+    d = load_nn("nn_dqn_update")
+    q = DQNDeepSetAgent(8).to(device)
+    q.load_state_dict(state_dict_from(d, "init__"))
+    tgt = DQNDeepSetAgent(8).to(device)
+    tgt.load_state_dict(state_dict_from(d, "target__"))
+    f = lambda k, dt=torch.float32: torch.from_numpy(np.asarray(d[k])).to(device, dt)  # noqa: E731
+    loss, td, old = dqn_loss(q, tgt, f("obs"), f("actions", torch.long), f("next_obs"), f("rewards"), f("dones"),
+                             float(d["gamma"]))
+    t = tol(device)
+    close(td, d["td_target"], what="td target", **t)
+    close(old, d["old_val"], what="old val", **t)
+    close(loss, d["loss"], what="loss", **t)
+    opt = torch.optim.Adam(q.parameters(), lr=2.5e-4)
+    opt.zero_grad()
+    loss.backward()
+    gmax = max(np.abs(d["grad__" + n.replace(".", "__")]).max() for n, _ in q.named_parameters())
+    for n, p in q.named_parameters():
+        close(p.grad, d["grad__" + n.replace(".", "__")], what="grad " + n, rtol=t["rtol"] * 10,
+              atol=max(t["atol"] * 10, 1e-5 * gmax))
+    opt.step()
+    for n, p in q.state_dict().items():
+        close(p, d["after__" + n.replace(".", "__")], what="param " + n, rtol=1e-4, atol=1e-6)
+
+
+def test_state_dict_names_match_reference():
+    from lbk8s.deepsets import DeepSetAgent, DQNDeepSetAgent
+    d = load_nn("nn_forward_e8")
+    assert set(DeepSetAgent(8).state_dict()) == set(state_dict_from(d, "agent__"))
+    assert set(DQNDeepSetAgent(8).state_dict()) == set(state_dict_from(d, "qnet__"))
+    assert sum(p.numel() for p in DeepSetAgent(8).actor.parameters()) == 9344
+    assert sum(p.numel() for p in DeepSetAgent(8).critic.parameters()) == 21633
+
+
+def test_gae_matches_direct_recursion():
+    from lbk8s.ppo import compute_gae
+    g = torch.Generator().manual_seed(0)
+    T, B = 7, 5
+    r, v = torch.randn(T, B, generator=g), torch.randn(T, B, generator=g)
+    dn = (torch.rand(T, B, generator=g) < 0.2).float()
+    nv, nd = torch.randn(1, B, generator=g), (torch.rand(B, generator=g) < 0.2).float()
+    adv, ret = compute_gae(r, v, dn, nv, nd, 0.95, 0.97)
+    for b in range(B):
+        last = 0.0
+        for t in reversed(range(T)):
+            nnt = 1.0 - (nd[b] if t == T - 1 else dn[t + 1, b])
+            nval = nv[0, b] if t == T - 1 else v[t + 1, b]
+            delta = r[t, b] + 0.95 * nval * nnt - v[t, b]
+            last = delta + 0.95 * 0.97 * nnt * last
+            assert abs(adv[t, b] - last) < 1e-5
+    assert torch.allclose(ret, adv + v)
