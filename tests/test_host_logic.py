@@ -163,3 +163,40 @@ def test_sharding_invariance_oracle(oracle_mod):
         outs = [p.step(a[i * (B // 2):(i + 1) * (B // 2)]) for i, p in enumerate(parts)]
         np.testing.assert_array_equal(o1, np.concatenate([x[0] for x in outs]))
         np.testing.assert_array_equal(r1, np.concatenate([x[1] for x in outs]))
+
+
+def _allreduce_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from lbk8s.deepsets import DQNDeepSetAgent, allreduce_gradients
+    torch.manual_seed(0)
+    net = DQNDeepSetAgent(8)
+    x = torch.full((3, 9, 8), float(rank + 1))
+    net(x).sum().backward()
+    allreduce_gradients(net)
+    q.put((rank, torch.cat([p.grad.reshape(-1) for p in net.parameters()]).numpy()))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_gradient_allreduce():
+    """The learners' one-bucket gradient average over 2 ranks equals the mean of the
+    per-rank gradients (identical replicas afterwards)."""
+    from lbk8s.deepsets import DQNDeepSetAgent
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_allreduce_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    expect = []
+    for r in range(2):
+        torch.manual_seed(0)
+        net = DQNDeepSetAgent(8)
+        net(torch.full((3, 9, 8), float(r + 1))).sum().backward()
+        expect.append(torch.cat([p.grad.reshape(-1) for p in net.parameters()]).numpy())
+    mean = (expect[0] + expect[1]) / 2
+    np.testing.assert_allclose(out[0], mean, rtol=1e-6, atol=1e-7)
+    np.testing.assert_array_equal(out[0], out[1])
