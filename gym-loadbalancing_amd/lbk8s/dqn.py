@@ -102,6 +102,8 @@ class DQN_DeepSets:
         self._rew = torch.zeros(self.num_envs, device=self.device)
         self._next_obs = torch.zeros((self.num_envs,) + tuple(env.observation_space.shape), device=self.device)
         self.episode_returns = []
+        self._ep_sum = torch.zeros((), dtype=torch.float64, device=self.device)
+        self._ep_cnt = torch.zeros((), dtype=torch.float64, device=self.device)
         self.train_steps = 0
 
     def select_actions(self, obs, masks, epsilon):
@@ -139,16 +141,26 @@ class DQN_DeepSets:
             self._act.copy_(actions)
             env.step_device(self._act, obs_out=self._next_obs, reward_out=self._rew, done_out=self._done_u8)
             dones = self._done_u8.float()
-            if global_step % 100 == 0 and bool(self._done_u8.any()):
-                self.episode_returns.append(env.ep_stats[self._done_u8.bool(), 0].mean().item())
+            # finished-episode returns accumulate on the device (no per-step host sync)
+            self._ep_sum += (env.ep_stats[:, 0] * dones).sum()
+            self._ep_cnt += dones.sum()
             self.rb.add(obs, self._next_obs, actions, self._rew, dones)
             obs.copy_(self._next_obs)
             if global_step > self.learning_starts and global_step % self.train_frequency == 0:
                 loss = self.train_step(global_step)
-            if global_step % 1000 == 0:
+            if global_step % 1000 == 0 or global_step == total_timesteps - 1:
+                self._flush_returns()
                 self.log_fn(dict(global_step=global_step, epsilon=eps, sps=(global_step + 1) / (time.time() - start),
-                                 loss=None if loss is None else loss.item()))
+                                 loss=None if loss is None else loss.item(),
+                                 ep_return=self.episode_returns[-1] if self.episode_returns else float("nan")))
         return self
+
+    def _flush_returns(self):
+        n = float(self._ep_cnt.item())
+        if n > 0:
+            self.episode_returns.append(float(self._ep_sum.item()) / n)
+        self._ep_sum.zero_()
+        self._ep_cnt.zero_()
 
     def predict(self, obs, masks=None):
         with torch.no_grad():

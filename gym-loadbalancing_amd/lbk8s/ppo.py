@@ -102,6 +102,8 @@ class PPO_DeepSets:
         self._act = torch.zeros(B, dtype=torch.int32, device=dev)
         self._done_u8 = torch.zeros(B, dtype=torch.uint8, device=dev)
         self.episode_returns = []
+        self._ep_sum = torch.zeros((), dtype=torch.float64, device=dev)
+        self._ep_cnt = torch.zeros((), dtype=torch.float64, device=dev)
 
     def rollout(self, next_obs, next_done):
         """Fill the (T, B) storage; returns the obs/done that follow the last step."""
@@ -117,9 +119,14 @@ class PPO_DeepSets:
             env.step_device(self._act, obs_out=env.obs, reward_out=self.rewards[step], done_out=self._done_u8)
             next_obs = env.obs
             next_done = self._done_u8.float()
-            if bool(self._done_u8.any()):
-                d = self._done_u8.bool()
-                self.episode_returns.append(env.ep_stats[d, 0].mean().item())
+            # finished-episode returns accumulate on the device (no per-step host sync)
+            self._ep_sum += (env.ep_stats[:, 0] * next_done).sum()
+            self._ep_cnt += next_done.sum()
+        n = float(self._ep_cnt.item())
+        if n > 0:
+            self.episode_returns.append(float(self._ep_sum.item()) / n)
+        self._ep_sum.zero_()
+        self._ep_cnt.zero_()
         return next_obs, next_done
 
     def update(self, next_obs, next_done):
