@@ -70,8 +70,11 @@ def test_ppo_minibatch_update_matches_reference(device):
     gn = torch.nn.utils.clip_grad_norm_(agent.parameters(), 0.5)
     close(gn, d["grad_norm"], what="grad norm", **t)
     opt.step()
+    # Adam rescales each gradient by its own magnitude: entries whose gradient is rounding
+    # noise (see above) move by up to lr; on the GPU allow 5% of lr on those
+    patol = 1e-6 if device == "cpu" else 0.05 * 2.5e-4
     for n, p in agent.state_dict().items():
-        close(p, d["after__" + n.replace(".", "__")], what="param " + n, rtol=1e-4, atol=1e-6)
+        close(p, d["after__" + n.replace(".", "__")], what="param " + n, rtol=1e-4, atol=patol)
 
 
 @pytest.mark.parametrize("device", DEVICES)
@@ -98,8 +101,9 @@ def test_dqn_train_step_matches_reference(device):
         close(p.grad, d["grad__" + n.replace(".", "__")], what="grad " + n, rtol=t["rtol"] * 10,
               atol=max(t["atol"] * 10, 1e-5 * gmax))
     opt.step()
+    patol = 1e-6 if device == "cpu" else 0.05 * 2.5e-4
     for n, p in q.state_dict().items():
-        close(p, d["after__" + n.replace(".", "__")], what="param " + n, rtol=1e-4, atol=1e-6)
+        close(p, d["after__" + n.replace(".", "__")], what="param " + n, rtol=1e-4, atol=patol)
 
 
 def test_state_dict_names_match_reference():
