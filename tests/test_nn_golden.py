@@ -11,6 +11,22 @@ import torch
 from nn_helpers import close, load_nn, state_dict_from
 
 DEVICES = ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
+LR = 2.5e-4
+
+
+def check_adam_step(module, d, gmax, device):
+    """Parameters after one Adam step.  The first Adam step moves every entry by
+    lr * g / (|g| + eps), i.e. by at most lr; where |g| is at the rounding-noise level
+    (the true gradient is ~0) the direction is not reproducible across devices, so those
+    entries are only bounded by lr, and the entries with a real gradient must match."""
+    for n, p in module.named_parameters():
+        key = n.replace(".", "__")
+        got = p.detach().cpu().numpy()
+        exp, init, g = d["after__" + key], d["init__" + key], np.abs(d["grad__" + key])
+        assert np.all(np.abs(got - init) <= LR * 1.001), n
+        real = g > (1e-6 if device == "cpu" else 1e-3) * gmax
+        np.testing.assert_allclose(got[real], exp[real], rtol=1e-4, atol=1e-6 if device == "cpu" else 2e-6,
+                                   err_msg="param " + n)
 
 
 def tol(device):
@@ -70,11 +86,7 @@ def test_ppo_minibatch_update_matches_reference(device):
     gn = torch.nn.utils.clip_grad_norm_(agent.parameters(), 0.5)
     close(gn, d["grad_norm"], what="grad norm", **t)
     opt.step()
-    # Adam rescales each gradient by its own magnitude: entries whose gradient is rounding
-    # noise (see above) move by up to lr; on the GPU allow 5% of lr on those
-    patol = 1e-6 if device == "cpu" else 0.05 * 2.5e-4
-    for n, p in agent.state_dict().items():
-        close(p, d["after__" + n.replace(".", "__")], what="param " + n, rtol=1e-4, atol=patol)
+    check_adam_step(agent, d, gmax, device)
 
 
 @pytest.mark.parametrize("device", DEVICES)
@@ -101,9 +113,7 @@ def test_dqn_train_step_matches_reference(device):
         close(p.grad, d["grad__" + n.replace(".", "__")], what="grad " + n, rtol=t["rtol"] * 10,
               atol=max(t["atol"] * 10, 1e-5 * gmax))
     opt.step()
-    patol = 1e-6 if device == "cpu" else 0.05 * 2.5e-4
-    for n, p in q.state_dict().items():
-        close(p, d["after__" + n.replace(".", "__")], what="param " + n, rtol=1e-4, atol=patol)
+    check_adam_step(q, d, gmax, device)
 
 
 def test_state_dict_names_match_reference():
