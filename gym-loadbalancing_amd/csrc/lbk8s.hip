@@ -14,11 +14,13 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 
 #include "lbk8s.h"
 #include "lbk8s_common.h"
+#include "lbk8s_deepsets.h"
 #include "lbk8s_slice.h"
 #include "lbk8s_tpe.h"
 
@@ -327,6 +329,17 @@ unsigned slice_blocks(int64_t B, int W) {
 }
 unsigned env_blocks(int64_t B) { return (unsigned)((B + BLOCK - 1) / BLOCK); }
 
+int device_cus() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+    }
+    return cus;
+}
+
 }  // namespace lbk
 
 using namespace lbk;
@@ -459,6 +472,37 @@ int lb_status(const void* state, const lb_config* cfg, int64_t num_envs, uint32_
     hipStream_t s = (hipStream_t)stream;
     if (hipMemsetAsync(flags_out, 0, sizeof(uint32_t), s) != hipSuccess) return fail("hipMemsetAsync failed");
     hipLaunchKernelGGL(k_status, dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p, flags_out);
+    return check_launch();
+}
+
+int lb_ds_pack(const lb_ds_weights* w, float* frag_out, void* stream) {
+    if (!w || !frag_out) return fail("weights/frag_out NULL");
+    for (int i = 0; i < 3; ++i)
+        if (!w->actor_lambda[i] || !w->actor_gamma[i]) return fail("actor weights are required");
+    hipLaunchKernelGGL(k_ds_pack, dim3((DS_FLOATS + 255) / 256), dim3(256), 0, (hipStream_t)stream, *w, frag_out);
+    return check_launch();
+}
+
+int lb_ds_forward(const float* frag, const float* obs, int64_t num_envs, int32_t num_elements, float* logits_out,
+                  float* value_out, void* stream) {
+    static_assert(DS_FLOATS == LB_DS_FRAG_FLOATS, "fragment layout and header disagree");
+    if (!frag || !obs || num_envs < 1) return fail("frag/obs NULL or num_envs < 1");
+    if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS)
+        return fail("num_elements must be in [1, 80] (LB_DS_MAX_ELEMENTS)");
+    if (!logits_out && !value_out) return 0;
+    DSParams p{obs, frag, logits_out, value_out, num_envs, num_elements, logits_out != nullptr, value_out != nullptr};
+    // persistent blocks (the 132 KiB weight image is staged once per block), one env per
+    // wave iteration
+    const int64_t want = (num_envs + DS_BLOCK / 64 - 1) / (DS_BLOCK / 64);
+    const unsigned grid = (unsigned)std::min<int64_t>(want, device_cus());
+    hipStream_t s = (hipStream_t)stream;
+    switch ((num_elements + 15) / 16) {
+        case 1: hipLaunchKernelGGL(k_deepsets_fwd<1>, dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        case 2: hipLaunchKernelGGL(k_deepsets_fwd<2>, dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        case 3: hipLaunchKernelGGL(k_deepsets_fwd<3>, dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        case 4: hipLaunchKernelGGL(k_deepsets_fwd<4>, dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        default: hipLaunchKernelGGL(k_deepsets_fwd<5>, dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+    }
     return check_launch();
 }
 

@@ -42,6 +42,17 @@ class LBTraceC(C.Structure):
     _fields_ = [(f, C.c_void_p) for f in TRACE_FIELDS]
 
 
+class LBDSWeightsC(C.Structure):
+    """struct lb_ds_weights: device pointers to the torch parameters, as they are."""
+    _fields_ = [("actor_lambda", C.c_void_p * 3), ("actor_gamma", C.c_void_p * 3),
+                ("critic_lambda", C.c_void_p * 3), ("critic_gamma", C.c_void_p * 3),
+                ("rho_w1", C.c_void_p), ("rho_b1", C.c_void_p), ("rho_w2", C.c_void_p),
+                ("rho_b2", C.c_void_p)]
+
+
+LB_DS_FRAG_FLOATS = 33860
+LB_DS_MAX_ELEMENTS = 80
+
 _lib = None
 
 
@@ -74,8 +85,10 @@ def lib():
     L.lb_get_field.argtypes = [vp, cfgp, i64, i32, vp, vp]
     L.lb_get_stats.argtypes = [vp, cfgp, i64, vp, vp]
     L.lb_status.argtypes = [vp, cfgp, i64, vp, vp]
+    L.lb_ds_pack.argtypes = [C.POINTER(LBDSWeightsC), vp, vp]
+    L.lb_ds_forward.argtypes = [vp, vp, i64, i32, vp, vp, vp]
     for f in ("lb_validate_config", "lb_state_bytes", "lb_init", "lb_reset", "lb_step", "lb_policy",
-              "lb_get_field", "lb_get_stats", "lb_status"):
+              "lb_get_field", "lb_get_stats", "lb_status", "lb_ds_pack", "lb_ds_forward"):
         getattr(L, f).restype = C.c_int
     v = L.lb_abi_version()
     if v != ABI_VERSION:
@@ -96,4 +109,4 @@ def check(rc):
 
 EXPORTED_SYMBOLS = ("lb_abi_version", "lb_last_error", "lb_validate_config", "lb_state_bytes",
                     "lb_init", "lb_reset", "lb_step", "lb_policy", "lb_get_field", "lb_get_stats",
-                    "lb_status")
+                    "lb_status", "lb_ds_pack", "lb_ds_forward")

@@ -21,6 +21,7 @@ import torch
 import torch.nn.functional as F
 from torch import optim
 
+from . import fused
 from .deepsets import DQNDeepSetAgent, HUGE_NEG, allreduce_gradients
 
 
@@ -66,7 +67,7 @@ class DeviceReplayBuffer:
 def dqn_loss(q_network, target_network, obs, actions, next_obs, rewards, dones, gamma):
     """dqn_deepset.py:180-187 -> (loss, td_target, old_val)."""
     with torch.no_grad():
-        target_max, _ = target_network(next_obs).max(dim=1)
+        target_max, _ = fused.q_forward(target_network, next_obs).max(dim=1)
         td_target = rewards.flatten() + gamma * target_max * (1 - dones.flatten())
     old_val = q_network(obs).gather(1, actions).squeeze()
     return F.mse_loss(td_target, old_val), td_target, old_val
@@ -111,7 +112,7 @@ class DQN_DeepSets:
             probs = masks.float()
             return torch.multinomial(probs, 1, generator=self.gen).squeeze(-1)
         with torch.no_grad():
-            q = torch.where(masks, self.q_network(obs), torch.full((), HUGE_NEG, device=obs.device))
+            q = torch.where(masks, fused.q_forward(self.q_network, obs), torch.full((), HUGE_NEG, device=obs.device))
         return torch.argmax(q, dim=1)
 
     def train_step(self, global_step):

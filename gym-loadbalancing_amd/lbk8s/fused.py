@@ -1,12 +1,115 @@
-"""Dispatch for the fused deep-sets forward (actor logits + critic value in one launch).
+"""Fused deep-sets forward: lb_ds_forward in liblbk8s.so.
 
-Until the HIP kernel lb_ds_forward is selected (lbk8s.fused.ENABLED), the two torch
-modules run (on the same device as the inputs); both paths return (logits (B,R), value (B,)).
+The reference evaluates its policy with torch modules (envs/deep_sets_agent_original.py:
+56-106; the DQN Q network, envs/deep_sets_agent_dqn.py:10-42).  Rollouts here call one
+HIP kernel per step instead: it reads each env's (R, 8) observation once and writes the
+R actor logits (or Q values) and the critic value, every layer on f32 MFMA with the
+activations kept in registers (csrc/lbk8s_deepsets.h).
+
+The kernel takes the weights in fragment order; `lb_ds_pack` builds that image from the
+torch parameters on the device.  The image is cached per module and rebuilt when any
+parameter's version counter moves (every optimizer step bumps it), so callers never
+repack by hand.
+
+Training (the PPO / DQN losses) keeps the torch modules: autograd needs them.  Inputs the
+kernel does not cover (not on a HIP device, R > 80, non-reference widths) run the same
+torch modules on the same device; `require=True` turns that into an error instead.
 """
+import ctypes as C
+import weakref
+
 import torch
 
-ENABLED = False
+from . import _native
+
+ENABLED = True
+_cache = weakref.WeakKeyDictionary()
 
 
-def deepsets_forward(agent, x: torch.Tensor):
-    return agent.actor(x), agent.critic(x)
+def _ptr(t):
+    return t.data_ptr() if t is not None else None
+
+
+def _weights_struct(actor_net, critic):
+    w = _native.LBDSWeightsC()
+    keep = []
+
+    def put(t):
+        t = t.detach().float().contiguous()
+        keep.append(t)
+        return t.data_ptr()
+
+    for i, j in enumerate((0, 2, 4)):
+        w.actor_lambda[i] = put(actor_net[j].Lambda.weight)
+        w.actor_gamma[i] = put(actor_net[j].Gamma.weight)
+    if critic is not None:
+        for i, j in enumerate((0, 2, 4)):
+            w.critic_lambda[i] = put(critic.psi[j].Lambda.weight)
+            w.critic_gamma[i] = put(critic.psi[j].Gamma.weight)
+        w.rho_w1 = put(critic.rho[0].weight)
+        w.rho_b1 = put(critic.rho[0].bias)
+        w.rho_w2 = put(critic.rho[2].weight)
+        w.rho_b2 = put(critic.rho[2].bias)
+    return w, keep
+
+
+def _geometry_ok(actor_net, x):
+    return (x.is_cuda and x.dim() == 3 and x.shape[-1] == 8 and 1 <= x.shape[1] <= _native.LB_DS_MAX_ELEMENTS
+            and actor_net[0].Lambda.weight.shape == (64, 8) and actor_net[2].Lambda.weight.shape == (64, 64))
+
+
+def packed(module, actor_net, critic):
+    """Fragment image of (actor_net, critic) cached on `module`; rebuilt after any update."""
+    params = list(actor_net.parameters()) + (list(critic.parameters()) if critic is not None else [])
+    version = tuple(p._version for p in params) + tuple(p.data_ptr() for p in params)
+    hit = _cache.get(module)
+    if hit is not None and hit[0] == version:
+        return hit[1]
+    dev = params[0].device
+    frag = torch.empty(_native.LB_DS_FRAG_FLOATS, dtype=torch.float32, device=dev)
+    w, keep = _weights_struct(actor_net, critic)
+    L = _native.lib()
+    _native.check(L.lb_ds_pack(C.byref(w), frag.data_ptr(), torch.cuda.current_stream(dev).cuda_stream))
+    del keep  # stream-ordered: the pack kernel is enqueued before any later reuse of the memory
+    _cache[module] = (version, frag)
+    return frag
+
+
+def _launch(frag, x, logits, value):
+    L = _native.lib()
+    B, R, _ = x.shape
+    _native.check(L.lb_ds_forward(frag.data_ptr(), x.data_ptr(), B, R, _ptr(logits), _ptr(value),
+                                  torch.cuda.current_stream(x.device).cuda_stream))
+
+
+@torch.no_grad()
+def deepsets_forward(agent, x: torch.Tensor, require: bool = False):
+    """(logits (B, R), value (B,)) of a DeepSetAgent, in one launch when possible."""
+    actor_net = agent.actor.net
+    if not (ENABLED and _geometry_ok(actor_net, x)):
+        if require:
+            raise RuntimeError(f"fused deep-sets forward does not cover input {tuple(x.shape)} on {x.device}")
+        return agent.actor(x), agent.critic(x)
+    x = x.float().contiguous()
+    frag = packed(agent, actor_net, agent.critic)
+    B, R, _ = x.shape
+    logits = torch.empty((B, R), dtype=torch.float32, device=x.device)
+    value = torch.empty((B,), dtype=torch.float32, device=x.device)
+    _launch(frag, x, logits, value)
+    return logits, value
+
+
+@torch.no_grad()
+def q_forward(qnet, x: torch.Tensor, require: bool = False):
+    """Q values (B, R) of a DQNDeepSetAgent (actor-only image of its q_network)."""
+    net = qnet.q_network.net
+    if not (ENABLED and _geometry_ok(net, x)):
+        if require:
+            raise RuntimeError(f"fused deep-sets forward does not cover input {tuple(x.shape)} on {x.device}")
+        return qnet.q_network(x)
+    x = x.float().contiguous()
+    frag = packed(qnet, net, None)
+    B, R, _ = x.shape
+    q = torch.empty((B, R), dtype=torch.float32, device=x.device)
+    _launch(frag, x, q, None)
+    return q
