@@ -491,17 +491,20 @@ int lb_ds_forward(const float* frag, const float* obs, int64_t num_envs, int32_t
         return fail("num_elements must be in [1, 80] (LB_DS_MAX_ELEMENTS)");
     if (!logits_out && !value_out) return 0;
     DSParams p{obs, frag, logits_out, value_out, num_envs, num_elements, logits_out != nullptr, value_out != nullptr};
-    // persistent blocks (the 132 KiB weight image is staged once per block), one env per
-    // wave iteration
-    const int64_t want = (num_envs + DS_BLOCK / 64 - 1) / (DS_BLOCK / 64);
+    // persistent blocks (the 132 KiB weight image is staged once per block); a wave takes
+    // P envs per iteration: P = 4 for R <= 16, 2 for R <= 32, else 1
+    const int ts = (num_elements + 15) / 16;
+    const int P = ts == 1 ? 4 : (ts == 2 ? 2 : 1);
+    const int64_t groups = (num_envs + P - 1) / P;
+    const int64_t want = (groups + DS_BLOCK / 64 - 1) / (DS_BLOCK / 64);
     const unsigned grid = (unsigned)std::min<int64_t>(want, device_cus());
     hipStream_t s = (hipStream_t)stream;
-    switch ((num_elements + 15) / 16) {
-        case 1: hipLaunchKernelGGL(k_deepsets_fwd<1>, dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
-        case 2: hipLaunchKernelGGL(k_deepsets_fwd<2>, dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
-        case 3: hipLaunchKernelGGL(k_deepsets_fwd<3>, dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
-        case 4: hipLaunchKernelGGL(k_deepsets_fwd<4>, dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
-        default: hipLaunchKernelGGL(k_deepsets_fwd<5>, dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+    switch (ts) {
+        case 1: hipLaunchKernelGGL((k_deepsets_fwd<1, 4>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        case 2: hipLaunchKernelGGL((k_deepsets_fwd<2, 2>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        case 3: hipLaunchKernelGGL((k_deepsets_fwd<3, 1>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        case 4: hipLaunchKernelGGL((k_deepsets_fwd<4, 1>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        default: hipLaunchKernelGGL((k_deepsets_fwd<5, 1>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
     }
     return check_launch();
 }

@@ -13,7 +13,8 @@
 // k-step), and staged once per block in LDS.  The set-wise max of a layer input is a
 // 16-lane max over the lanes of one lane group (plus an elementwise max over set tiles);
 // replicated over the 16 columns it is the B operand of the Gamma pass, whose result
-// (every column equal) initialises the accumulator: acc = -Gamma·max + Lambda·H.
+// (every column equal) initialises the accumulator: acc = (-Gamma)·max + Lambda·H, with
+// -Gamma stored by the pack kernel.
 // Invalid set columns (padding past R) are excluded from the max and the mean.
 #pragma once
 
@@ -47,66 +48,133 @@ enum : int {
     DS_R1W = 28672, DS_R1B = 32768, DS_R2W = 32832, DS_R2B = 33856, DS_FLOATS = 33860,
 };
 
-constexpr int DS_BLOCK = 512;       // 8 waves: 2 per SIMD
+constexpr int DS_BLOCK = 512;             // 8 waves: 2 per SIMD
 constexpr int DS_LDS_FLOATS = DS_FLOATS;  // 132 KiB of weight fragments: one block per CU
 
 __device__ __forceinline__ dsf4 mfma4(float a, float b, dsf4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-__device__ __forceinline__ float group_max16(float v) {
-#pragma unroll
-    for (int m = 8; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
-    return v;
-}
-__device__ __forceinline__ float group_sum16(float v) {
-#pragma unroll
-    for (int m = 8; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-    return v;
-}
+// DPP inside a 16-lane row.  Reductions (max / sum over the 16 lanes, every lane gets the
+// result) are quad_perm xor 1, xor 2, row_ror 4, row_ror 8, written as v_max/v_add with the
+// DPP operand so there is no separate move; four independent values per asm block keep three
+// VALU ops between a write and its DPP read (the hazard needs two wait states), and the
+// leading s_nop covers whatever the compiler scheduled just before the block.
+#define LBK_DPP4(OP, CTRL)                                                              \
+    OP " %0, %0, %0 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"             \
+    OP " %1, %1, %1 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"             \
+    OP " %2, %2, %2 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"             \
+    OP " %3, %3, %3 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+#define LBK_ROW_REDUCE4(OP)                                                             \
+    asm volatile("s_nop 1\n\t" LBK_DPP4(OP, "quad_perm:[1,0,3,2]") LBK_DPP4(OP, "quad_perm:[2,3,0,1]") \
+                 LBK_DPP4(OP, "row_ror:4") LBK_DPP4(OP, "row_ror:8")                    \
+                 : "+v"(a), "+v"(b), "+v"(c), "+v"(d))
 
-__device__ __forceinline__ float act_elu(float x) { return x > 0.f ? x : expm1f(x); }
-__device__ __forceinline__ float act_relu(float x) { return x > 0.f ? x : 0.f; }
+__device__ __forceinline__ void row_max4(float& a, float& b, float& c, float& d) { LBK_ROW_REDUCE4("v_max_f32_dpp"); }
+__device__ __forceinline__ void row_sum4(float& a, float& b, float& c, float& d) { LBK_ROW_REDUCE4("v_add_f32_dpp"); }
 
-// set-wise max of a fragment set: per k-step, max over valid columns of every set tile,
-// then over the 16 lanes of the lane group -> the value replicated in every column
-template <int TS, int KS>
-__device__ __forceinline__ void set_max(const float (&h)[TS][KS], float (&mx)[KS], int lane, int R) {
+// reduce N values in place, four per block (the tail padded with scratch values)
+template <bool MAX, int N>
+__device__ __forceinline__ void row_reduce(float (&v)[N]) {
 #pragma unroll
-    for (int k = 0; k < KS; ++k) {
-        float v = -INFINITY;
-#pragma unroll
-        for (int s = 0; s < TS; ++s)
-            if (16 * s + (lane & 15) < R) v = fmaxf(v, h[s][k]);
-        mx[k] = group_max16(v);
+    for (int i = 0; i < N; i += 4) {
+        float x0 = v[i], x1 = i + 1 < N ? v[i + 1] : 0.f, x2 = i + 2 < N ? v[i + 2] : 0.f,
+              x3 = i + 3 < N ? v[i + 3] : 0.f;
+        if (MAX) row_max4(x0, x1, x2, x3);
+        else row_sum4(x0, x1, x2, x3);
+        v[i] = x0;
+        if (i + 1 < N) v[i + 1] = x1;
+        if (i + 2 < N) v[i + 2] = x2;
+        if (i + 3 < N) v[i + 3] = x3;
     }
 }
 
-// one equivariant layer with 64 outputs: out = act(Lambda·h - Gamma·max_set(h))
-// KS = input k-steps (2 for the 8-feature obs, 16 for 64 features)
-template <int TS, int KS, int ACT>
-__device__ __forceinline__ void eq_layer64(const float* L, const float* G, const float (&h)[TS][KS],
-                                           const float (&mx)[KS], float (&out)[TS][16], int lane) {
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float max2(float a, float b) { return a > b ? a : b; }
+// value of column S of this lane's 16-lane row (row_newbcast)
+template <int S>
+__device__ __forceinline__ float from_col(float v) { return dpp<0x150 + S>(v); }
+
+// broadcast from column s (s a loop index of a fully unrolled loop over P <= 4)
+template <int P>
+__device__ __forceinline__ float from_col_dyn(float v, int s) {
+    if (P == 1) return v;  // every column of a single env's result is equal
+    switch (s) {
+        case 0: return from_col<0>(v);
+        case 1: return from_col<1>(v);
+        case 2: return from_col<2>(v);
+        default: return from_col<3>(v);
+    }
+}
+
+// ELU(alpha=1) without a divergent branch: exp2 on the clamped argument
+__device__ __forceinline__ float act_elu(float x) {
+    const float e = __builtin_amdgcn_exp2f(fminf(x, 0.f) * 1.4426950408889634f) - 1.0f;
+    return x > 0.f ? x : e;
+}
+__device__ __forceinline__ float act_relu(float x) { return x > 0.f ? x : 0.f; }
+
+// A wave iteration holds P envs of TS set tiles each: fragment array h[P*TS][KS], tile
+// (s, t) = env s, set elements 16t..16t+15.  Per-env reductions (max, mean) run over that
+// env's valid columns; the Gamma pass and rho are BATCHED over the P envs: column c of their
+// B operand carries env (c mod P), and each env's result is broadcast back from its column.
+// batched B operand of the Gamma pass: per k-step, env (col mod P)'s set-wise max
+template <int TS, int P, int KS>
+__device__ __forceinline__ void set_max_batched(const float (&h)[P * TS][KS], float (&mb)[KS], int col, int R) {
+    float m[KS * P];
+#pragma unroll
+    for (int k = 0; k < KS; ++k)
+#pragma unroll
+        for (int s = 0; s < P; ++s) {
+            float v = -INFINITY;
+#pragma unroll
+            for (int t = 0; t < TS; ++t)
+                if (16 * t + col < R) v = max2(v, h[s * TS + t][k]);
+            m[k * P + s] = v;
+        }
+    row_reduce<true>(m);
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+        float r = m[k * P];
+#pragma unroll
+        for (int s = 1; s < P; ++s) r = (col % P == s) ? m[k * P + s] : r;
+        mb[k] = r;
+    }
+}
+
+// out = act(Lambda·h - Gamma·max_set(h)), NT 16-row output tiles (4 for 64 outputs)
+template <int TS, int P, int KS, int ACT>
+__device__ __forceinline__ void eq_layer(const float* L, const float* G, const float (&h)[P * TS][KS],
+                                         const float (&mb)[KS], float (&out)[P * TS][16], int lane) {
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
         dsf4 g = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int k = 0; k < KS; ++k) g = mfma4(G[(nt * KS + k) * 64 + lane], mx[k], g);
+        for (int k = 0; k < KS; ++k) g = mfma4(G[(nt * KS + k) * 64 + lane], mb[k], g);
 #pragma unroll
-        for (int s = 0; s < TS; ++s) {
-            dsf4 acc = -g;
+        for (int s = 0; s < P; ++s) {
+            dsf4 init;
 #pragma unroll
-            for (int k = 0; k < KS; ++k) acc = mfma4(L[(nt * KS + k) * 64 + lane], h[s][k], acc);
+            for (int i = 0; i < 4; ++i) init[i] = from_col_dyn<P>(g[i], s);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                float x = acc[i];
-                out[s][4 * nt + i] = ACT == 1 ? act_relu(x) : (ACT == 2 ? act_elu(x) : x);
+            for (int t = 0; t < TS; ++t) {
+                dsf4 acc = init;
+#pragma unroll
+                for (int k = 0; k < KS; ++k) acc = mfma4(L[(nt * KS + k) * 64 + lane], h[s * TS + t][k], acc);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float x = acc[i];
+                    out[s * TS + t][4 * nt + i] = ACT == 1 ? act_relu(x) : (ACT == 2 ? act_elu(x) : x);
+                }
             }
         }
     }
 }
 
-template <int TS>
+template <int TS, int P>
 __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
     __shared__ __attribute__((aligned(16))) float W[DS_LDS_FLOATS];
     // stage the weight fragments (once per block; blocks are persistent)
@@ -118,56 +186,81 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
     const int64_t nwaves = (int64_t)gridDim.x * (DS_BLOCK / 64);
     const int R = p.R;
     const int col = lane & 15, grp = lane >> 4;
-    for (int64_t env = wave; env < p.B; env += nwaves) {
+    const int64_t groups = (p.B + P - 1) / P;
+    for (int64_t gi = wave; gi < groups; gi += nwaves) {
+        const int64_t env0 = gi * P;
         // obs -> layer-1 B fragments: k-step kk holds feature 4kk + grp of set element col
-        const float* x = p.obs + env * (int64_t)R * 8;
-        float h0[TS][2];
+        float h0[P * TS][2];
 #pragma unroll
-        for (int s = 0; s < TS; ++s) {
-            const int row = 16 * s + col;
+        for (int s = 0; s < P; ++s) {
+            const bool live = env0 + s < p.B;
+            const float* x = p.obs + (env0 + s) * (int64_t)R * 8;
 #pragma unroll
-            for (int kk = 0; kk < 2; ++kk) h0[s][kk] = row < R ? x[row * 8 + 4 * kk + grp] : 0.f;
+            for (int t = 0; t < TS; ++t) {
+                const int row = 16 * t + col;
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk) h0[s * TS + t][kk] = (live && row < R) ? x[row * 8 + 4 * kk + grp] : 0.f;
+            }
         }
         float m0[2];
-        set_max<TS, 2>(h0, m0, lane, R);
+        set_max_batched<TS, P, 2>(h0, m0, col, R);
 
-        float h1[TS][16], m1[16], h2[TS][16], m2[16];
+        float h1[P * TS][16], m1[16], h2[P * TS][16], m2[16];
         // ---- actor: Eq(8->64) ReLU Eq(64->64) ELU Eq(64->1)
         if (p.actor) {
-            eq_layer64<TS, 2, 1>(W + DS_A1L, W + DS_A1G, h0, m0, h1, lane);
-            set_max<TS, 16>(h1, m1, lane, R);
-            eq_layer64<TS, 16, 2>(W + DS_A2L, W + DS_A2G, h1, m1, h2, lane);
-            set_max<TS, 16>(h2, m2, lane, R);
+            eq_layer<TS, P, 2, 1>(W + DS_A1L, W + DS_A1G, h0, m0, h1, lane);
+            set_max_batched<TS, P, 16>(h1, m1, col, R);
+            eq_layer<TS, P, 16, 2>(W + DS_A2L, W + DS_A2G, h1, m1, h2, lane);
+            set_max_batched<TS, P, 16>(h2, m2, col, R);
             const float* L = W + DS_A3L;
             const float* G = W + DS_A3G;
             dsf4 g = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int k = 0; k < 16; ++k) g = mfma4(G[k * 64 + lane], m2[k], g);
 #pragma unroll
-            for (int s = 0; s < TS; ++s) {
-                dsf4 acc = -g;
+            for (int s = 0; s < P; ++s) {
+                const float init = from_col_dyn<P>(g[0], s);
 #pragma unroll
-                for (int k = 0; k < 16; ++k) acc = mfma4(L[k * 64 + lane], h2[s][k], acc);
-                const int row = 16 * s + col;
-                if (grp == 0 && row < R) p.logits[env * R + row] = acc[0];  // output feature 0
+                for (int t = 0; t < TS; ++t) {
+                    dsf4 acc = {init, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) acc = mfma4(L[k * 64 + lane], h2[s * TS + t][k], acc);
+                    const int row = 16 * t + col;
+                    if (grp == 0 && row < R && env0 + s < p.B) p.logits[(env0 + s) * R + row] = acc[0];
+                }
             }
         }
         if (!p.critic) continue;
 
         // ---- critic: psi = Eq ELU Eq ELU Eq, mean over the set, rho = Linear ELU Linear
-        eq_layer64<TS, 2, 2>(W + DS_C1L, W + DS_C1G, h0, m0, h1, lane);
-        set_max<TS, 16>(h1, m1, lane, R);
-        eq_layer64<TS, 16, 2>(W + DS_C2L, W + DS_C2G, h1, m1, h2, lane);
-        set_max<TS, 16>(h2, m2, lane, R);
-        eq_layer64<TS, 16, 0>(W + DS_C3L, W + DS_C3G, h2, m2, h1, lane);
+        eq_layer<TS, P, 2, 2>(W + DS_C1L, W + DS_C1G, h0, m0, h1, lane);
+        set_max_batched<TS, P, 16>(h1, m1, col, R);
+        eq_layer<TS, P, 16, 2>(W + DS_C2L, W + DS_C2G, h1, m1, h2, lane);
+        set_max_batched<TS, P, 16>(h2, m2, col, R);
+        eq_layer<TS, P, 16, 0>(W + DS_C3L, W + DS_C3G, h2, m2, h1, lane);
+        // batched mean: column c carries env (c mod P)'s mean over its valid set elements
         float mean[16];
+        {
+            const float invR = 1.0f / (float)R;
+            float sm[16 * P];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            float v = 0.f;
+            for (int k = 0; k < 16; ++k)
 #pragma unroll
-            for (int s = 0; s < TS; ++s)
-                if (16 * s + col < R) v += h1[s][k];
-            mean[k] = group_sum16(v) / (float)R;
+                for (int s = 0; s < P; ++s) {
+                    float v = 0.f;
+#pragma unroll
+                    for (int t = 0; t < TS; ++t)
+                        if (16 * t + col < R) v += h1[s * TS + t][k];
+                    sm[k * P + s] = v;
+                }
+            row_reduce<false>(sm);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                float r = sm[k * P];
+#pragma unroll
+                for (int s = 1; s < P; ++s) r = (col % P == s) ? sm[k * P + s] : r;
+                mean[k] = r * invR;
+            }
         }
         float r1[16];
 #pragma unroll
@@ -183,7 +276,8 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
         dsf4 v = {W[DS_R2B], 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < 16; ++k) v = mfma4(W[DS_R2W + k * 64 + lane], r1[k], v);
-        if (lane == 0) p.value[env] = v[0];
+        // row 0 of the result: column c = env (c mod P)
+        if (grp == 0 && col < P && env0 + col < p.B) p.value[env0 + col] = v[0];
     }
 }
 
@@ -228,7 +322,9 @@ __global__ void k_ds_pack(lb_ds_weights w, float* out) {
         case 14: v = ds_frag_value(w.rho_w2, 1, 64, 16, idx); break;
         default: v = (w.rho_b2 && idx == 0) ? w.rho_b2[0] : 0.f; break;
     }
-    out[i] = v;
+    // Gamma fragments are stored negated: the kernel adds (-Gamma)·max
+    const bool gamma = r == 1 || r == 3 || r == 5 || r == 7 || r == 9 || r == 11;
+    out[i] = gamma ? -v : v;
 }
 
 }  // namespace lbk
