@@ -99,6 +99,7 @@ class PPO_DeepSets:
         self.rewards = torch.zeros((T, B), device=dev)
         self.dones = torch.zeros((T, B), device=dev)
         self.values = torch.zeros((T, B), device=dev)
+        self._last_obs = torch.zeros((B, R, 8), device=dev)  # obs after the last rollout step
         self._act = torch.zeros(B, dtype=torch.int32, device=dev)
         self._done_u8 = torch.zeros(B, dtype=torch.uint8, device=dev)
         self.episode_returns = []
@@ -108,16 +109,20 @@ class PPO_DeepSets:
     def rollout(self, next_obs, next_done):
         """Fill the (T, B) storage; returns the obs/done that follow the last step."""
         env = self.env
-        for step in range(self.num_steps):
-            self.obs[step].copy_(next_obs)
+        T = self.num_steps
+        if next_obs.data_ptr() != self.obs[0].data_ptr():
+            self.obs[0].copy_(next_obs)
+        next_obs = self.obs[0]
+        for step in range(T):
             self.dones[step] = next_done
             action, logprob, value = self.agent.act(next_obs, generator=self.gen)  # no masks (:169)
             self.values[step] = value
             self.actions[step] = action.float()
             self.logprobs[step] = logprob
             self._act.copy_(action)
-            env.step_device(self._act, obs_out=env.obs, reward_out=self.rewards[step], done_out=self._done_u8)
-            next_obs = env.obs
+            # the env writes the next observation straight into the next storage slot
+            next_obs = self.obs[step + 1] if step + 1 < T else self._last_obs
+            env.step_device(self._act, obs_out=next_obs, reward_out=self.rewards[step], done_out=self._done_u8)
             next_done = self._done_u8.float()
             # finished-episode returns accumulate on the device (no per-step host sync)
             self._ep_sum += (env.ep_stats[:, 0] * next_done).sum()
