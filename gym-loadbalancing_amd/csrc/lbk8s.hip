@@ -8,7 +8,8 @@
 //
 // Two step kernels share one state representation (lbk8s_common.h):
 //   * E <= 8 : k_step_tpe   — one lane per env, LDS-staged coalesced obs (lbk8s_tpe.h)
-//   * E >  8 : k_step_slice — one W-lane slice per env, lanes over endpoints (lbk8s_slice.h)
+//   * E >  8 : k_step_slice — one W-lane slice per env (4 envs per wave up to E = 64),
+//                             lanes over endpoints (lbk8s_slice.h)
 
 #include <hip/hip_runtime.h>
 
@@ -172,7 +173,15 @@ struct Geo {
     int W, EPL, EP, NZW;
 };
 
-Geo geometry(const lb_config* c) {
+// E > 8: W-lane slices.  Few envs (B < 32768): one env per wave (W = 16/32/64 by E), so
+// the launch still has thousands of waves; many envs: 4 envs per wave up to E = 64, so
+// the per-env scalar chain (Philox, logs, reward) is issued once per 4 envs and 4x more
+// envs are in flight per CU.  Measured at E = 64 (tools/ablate.py): 2^20 envs 1.45 ->
+// 1.00 ms per step, 4096 envs 8.9 vs 20.7 us.  Both shapes give the same EP = W * EPL
+// (the next power of two >= max(E, 16)), so the state layout does not depend on B.
+[[maybe_unused]] constexpr int64_t WIDE_SLICE_MAX_B = 32768;
+
+Geo geometry(const lb_config* c, int64_t B = 0) {
     Geo g;
     const int E = c->num_endpoints;
     g.tpe = E <= TPE_E;
@@ -181,8 +190,18 @@ Geo geometry(const lb_config* c) {
         g.EPL = 1;
         g.EP = E;
     } else {
-        g.W = E <= 16 ? 16 : E <= 32 ? 32 : 64;
-        g.EPL = E <= 64 ? 1 : E <= 128 ? 2 : 4;
+#ifdef LB_ABL_WIDE_SLICE
+        const bool wide = true;
+#else
+        const bool wide = B < WIDE_SLICE_MAX_B;
+#endif
+        if (wide) {
+            g.W = E <= 16 ? 16 : E <= 32 ? 32 : 64;
+            g.EPL = E <= 64 ? 1 : E <= 128 ? 2 : 4;
+        } else {
+            g.W = E <= 64 ? 16 : E <= 128 ? 32 : 64;
+            g.EPL = E <= 16 ? 1 : E <= 32 ? 2 : 4;
+        }
         g.EP = g.W * g.EPL;
     }
     g.NZW = (c->num_nodes + 31) / 32;
@@ -316,6 +335,9 @@ int check_launch() {
 #define LB_DISPATCH_SLICE(W_, EPL_, BODY)                                         \
     do {                                                                          \
         if (W_ == 16 && EPL_ == 1) { constexpr int W = 16, EPL = 1; BODY; }       \
+        else if (W_ == 16 && EPL_ == 2) { constexpr int W = 16, EPL = 2; BODY; }  \
+        else if (W_ == 16 && EPL_ == 4) { constexpr int W = 16, EPL = 4; BODY; }  \
+        else if (W_ == 32 && EPL_ == 4) { constexpr int W = 32, EPL = 4; BODY; }  \
         else if (W_ == 32 && EPL_ == 1) { constexpr int W = 32, EPL = 1; BODY; }  \
         else if (W_ == 64 && EPL_ == 1) { constexpr int W = 64, EPL = 1; BODY; }  \
         else if (W_ == 64 && EPL_ == 2) { constexpr int W = 64, EPL = 2; BODY; }  \
@@ -386,7 +408,7 @@ int lb_reset(void* state, const lb_config* cfg, int64_t num_envs, const uint8_t*
     if (tr) p.tr = *trace;
     p.obs = obs_out;
     p.reset_mask = reset_mask;
-    Geo g = geometry(cfg);
+    Geo g = geometry(cfg, num_envs);
     hipStream_t s = (hipStream_t)stream;
     if (g.tpe) {
         if (tr) hipLaunchKernelGGL(k_reset_tpe<true>, dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);
@@ -421,7 +443,7 @@ int lb_step(void* state, const lb_config* cfg, int64_t num_envs, const int32_t* 
     p.done = done_out;
     p.term_obs = terminal_obs_out;
     p.ep_stats = ep_stats_out;
-    Geo g = geometry(cfg);
+    Geo g = geometry(cfg, num_envs);
     hipStream_t s = (hipStream_t)stream;
     if (g.tpe) {
         if (tr) hipLaunchKernelGGL(k_step_tpe<true>, dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);

@@ -11,6 +11,12 @@
 
 namespace lbk {
 
+#ifdef LB_ABL_SLICE_OCC4
+#define LB_SLICE_OCC __attribute__((amdgpu_waves_per_eu(4)))
+#else
+#define LB_SLICE_OCC
+#endif
+
 template <int W>
 __device__ __forceinline__ int slice_sum(int v) {
 #pragma unroll
@@ -40,13 +46,12 @@ __device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int src) { return (uint
 template <int W>
 __device__ __forceinline__ double shfl_f64(double v, int src) { return __shfl(v, src, W); }
 
-template <int EPL, typename T>
+// a[k] for a runtime k, as a chain of selects over constant indices (a runtime-indexed
+// private array would be placed in scratch memory)
+template <int EPL, int I = EPL - 1, typename T>
 __device__ __forceinline__ T sel(const T (&a)[EPL], int k) {
-    T v = a[0];
-#pragma unroll
-    for (int i = 1; i < EPL; ++i)
-        if (k == i) v = a[i];
-    return v;
+    if constexpr (I == 0) return a[0];
+    else return k == I ? a[I] : sel<EPL, I - 1>(a, k);
 }
 
 // next_request()'s draws (:1132-1133, :1116, :1120).  Draw map: block (D_REQ_X) ->
@@ -165,7 +170,7 @@ __device__ __forceinline__ void slice_next_request(const Params& p, int64_t env,
 
 // reset() (:290-400) into registers, then the per-episode state stores.
 template <int W, int EPL, bool TRACE>
-__device__ void slice_reset(const Params& p, int64_t env, int lane, SEnv<EPL>& v) {
+__device__ __forceinline__ void slice_reset(const Params& p, int64_t env, int lane, SEnv<EPL>& v) {
     const uint32_t episode = (uint32_t)(v.acc3 >> 32) + 1;
     // nodes (:349-373): zone capacity and the 2-bit zone of every node, one 32-node word
     // at a time (lane l takes nodes l, l+W, ... of the word)
@@ -279,7 +284,7 @@ __global__ __launch_bounds__(BLOCK) void k_reset_slice(Params p) {
 
 // step() (:403-513) fused with next_request(), get_state(), reward, done and auto-reset.
 template <int W, int EPL, bool TRACE>
-__global__ __launch_bounds__(BLOCK) void k_step_slice(Params p) {
+__global__ __launch_bounds__(BLOCK) LB_SLICE_OCC void k_step_slice(Params p) {
     const int lane = threadIdx.x % W;
     const int64_t env = (int64_t)blockIdx.x * (BLOCK / W) + threadIdx.x / W;
     if (env >= p.B) return;
@@ -313,9 +318,20 @@ __global__ __launch_bounds__(BLOCK) void k_step_slice(Params p) {
     const double next_cpu = p.cpu_lut[(Mn) * CPU_ROWS + c0A];
 #pragma unroll
     for (int k = 0; k < EPL; ++k) {  // observed values of every endpoint
-        const double l = p.lat_lut[ed_j(v.ed[k]) * LAT_ROWS + (int)v.lat0[k]];
-        v.olat[k] = (float)(ed_j(v.ed[k]) == 0 ? v.lat0[k] : l);
-        v.ocpu[k] = (float)p.cpu_lut[ed_m(v.ed[k]) * CPU_ROWS + em_c0(v.em[k])];
+        // table rows 0 are the initial values: only endpoints selected this episode
+        // (j > 0) / refreshed (m > 0) gather from the LUTs
+        const int j = ed_j(v.ed[k]), m = ed_m(v.ed[k]);
+        double l = v.lat0[k], c = (double)em_c0(v.em[k]);
+#ifdef LB_ABL_ALWAYS_LUT
+        l = p.lat_lut[j * LAT_ROWS + (int)v.lat0[k]];
+        if (j == 0) l = v.lat0[k];
+        c = p.cpu_lut[m * CPU_ROWS + em_c0(v.em[k])];
+#else
+        if (j) l = p.lat_lut[j * LAT_ROWS + (int)v.lat0[k]];
+        if (m) c = p.cpu_lut[m * CPU_ROWS + em_c0(v.em[k])];
+#endif
+        v.olat[k] = (float)l;
+        v.ocpu[k] = (float)c;
     }
 
     // ---- take_action (:578-686)
@@ -345,12 +361,13 @@ __global__ __launch_bounds__(BLOCK) void k_step_slice(Params p) {
 #pragma unroll
         for (int k = 0; k < EPL; ++k) {
             int e = lane + k * W;
-            if (e == oA) v.ed[k] = (v.ed[k] & ~(0x3FFu << 20)) | ((uint32_t)Mn << 20);
-            if (e == ai) {
-                v.ed[k] = (v.ed[k] & (0x3FFu << 20)) | ((uint32_t)Mn << 10) | (uint32_t)jn;
-                v.olat[k] = (float)next_lat;
-                v.ocpu[k] = (float)next_cpu;
-            }
+            // unconditional select-stores: a conditional store per k lets the compiler
+            // fold them into one runtime-indexed store (and move the arrays to LDS)
+            const uint32_t edo = e == oA ? (v.ed[k] & ~(0x3FFu << 20)) | ((uint32_t)Mn << 20) : v.ed[k];
+            const bool hit = e == ai;
+            v.ed[k] = hit ? (edo & (0x3FFu << 20)) | ((uint32_t)Mn << 10) | (uint32_t)jn : edo;
+            v.olat[k] = hit ? (float)next_lat : v.olat[k];
+            v.ocpu[k] = hit ? (float)next_cpu : v.ocpu[k];
         }
         v.s.penalty = 0;
         reward = accept_reward(p, sel_lat, tl, sel_cpu, v.acc2, v.s.acc);

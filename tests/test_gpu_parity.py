@@ -116,3 +116,40 @@ def test_philox_mode_matches_oracle(oracle_mod, name):
     np.testing.assert_array_equal(env.field("current_time").cpu().numpy(), orc.field("t"))
     # actions < -E were issued above: the status word must say so
     assert env.status() & 1
+
+
+# Many envs (B >= 32768, E > 8) take the 4-envs-per-wave slice shape (W = 16 or 32 lanes
+# per env, 2 or 4 endpoints per lane); fewer envs take one env per wave.  Same check as
+# above at a size that selects the many-env shape, with short episodes so auto-resets run.
+MANY_CFGS = {
+    "e64_multi_l10": dict(num_endpoints=64, reward_function="multi", episode_length=10),
+    "e20_latency_l10": dict(num_endpoints=20, reward_function="latency", episode_length=10),
+    "e100_fair_norej_l10": dict(num_endpoints=100, reward_function="fairness", rejection_allowed=False,
+                                episode_length=10),
+}
+
+
+@pytest.mark.parametrize("name", sorted(MANY_CFGS))
+def test_philox_many_envs_matches_oracle(oracle_mod, name):
+    from lbk8s import LBVecEnv
+    cfg = MANY_CFGS[name]
+    B = 32768
+    seed = 99
+    env = LBVecEnv(B, seed=seed, **cfg)
+    orc = oracle_mod.OracleBatch(cfg, B, trace=False, seed=seed)
+    orc.init()
+    np.testing.assert_array_equal(env.reset(), orc.reset())
+    rng = np.random.default_rng(1)
+    A = env.action_space.n
+    E = env.cfg.num_endpoints
+    for s in range(2 * env.cfg.episode_length + 3):
+        a = rng.integers(-E, A, size=B).astype(np.int32)
+        o1, r1, d1, _ = env.step(a)
+        o2, r2, d2, t2, _ = orc.step(a)
+        np.testing.assert_array_equal(r1, r2, err_msg=f"reward step {s}")
+        np.testing.assert_array_equal(d1, d2, err_msg=f"done step {s}")
+        np.testing.assert_array_equal(o1, o2, err_msg=f"obs step {s}")
+        if d1.any():
+            np.testing.assert_array_equal(env.terminal_obs.cpu().numpy()[d1], t2[d1])
+    np.testing.assert_array_equal(env.field("avg_load_served").cpu().numpy(), orc.field("loads"))
+    assert env.status() == 0

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """A/B the perf-experiment builds of liblbk8s (tools/_build/liblbk8s_<variant>.so) in ONE
-process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24).  Default scenario,
-2^20 envs, obs ring 16.  Prints median/min ms per lb_step per variant."""
+process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24).  Obs ring 16.
+Prints median/min ms per lb_step per variant.
+
+    python tools/ablate.py [variants,comma,separated] [scenario (bench.CONFIGS)] [envs]"""
 import ctypes as C
 import json
 import os
@@ -28,9 +30,11 @@ def load(path):
 
 def main():
     names = sys.argv[1].split(",") if len(sys.argv) > 1 else ["base", "PLAIN_OBS", "NO_LUT", "NO_OBS", "NO_RNG", "ED_FULL", "NT_STATE", "NT_LOAD"]
-    B = 1 << 20
+    scenario = sys.argv[2] if len(sys.argv) > 2 else "default"
+    from bench import CONFIGS
+    B = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 20
     dev = torch.device("cuda", 0)
-    cfg = LBConfig()
+    cfg = LBConfig(**CONFIGS[scenario])
     c = cfg.to_c(seed=0)
     R, T = cfg.obs_rows, 16
     stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -69,7 +73,7 @@ def main():
             res[name].append(ev0.elapsed_time(ev1) / 40)
     for name in names:
         v = sorted(res[name])
-        print(json.dumps(dict(variant=name, median_ms=round(v[len(v) // 2], 5), min_ms=round(v[0], 5),
+        print(json.dumps(dict(variant=name, scenario=scenario, envs=B, median_ms=round(v[len(v) // 2], 5), min_ms=round(v[0], 5),
                               env_steps_per_s=B / v[len(v) // 2] * 1e3)))
 
 
