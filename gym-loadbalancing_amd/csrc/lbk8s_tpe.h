@@ -298,11 +298,19 @@ __global__ __launch_bounds__(BLOCK) void k_step_tpe(Params p) {
 #ifdef LB_ABL_NO_LUT
             const double l = lat0[e];
             const double c = (double)em_c0(em[e]);
-#else
-            const double l = p.lat_lut[(j) * LAT_ROWS + (int)lat0[e]];
+#elif defined(LB_ABL_ALWAYS_LUT)
+            double l = p.lat_lut[(j) * LAT_ROWS + (int)lat0[e]];
+            if (j == 0) l = lat0[e];
             const double c = p.cpu_lut[ed_m(ed[e]) * CPU_ROWS + em_c0(em[e])];
+#else
+            // table rows 0 are the initial values: only endpoints selected (j > 0) /
+            // refreshed (m > 0) this episode gather from the LUTs
+            const int m = ed_m(ed[e]);
+            double l = lat0[e], c = (double)em_c0(em[e]);
+            if (j) l = p.lat_lut[j * LAT_ROWS + (int)lat0[e]];
+            if (m) c = p.cpu_lut[m * CPU_ROWS + em_c0(em[e])];
 #endif
-            float ol = j == 0 ? (float)lat0[e] : (float)l;
+            float ol = (float)l;
             float oc = (float)c;
             if (accept && e == ai) { ol = (float)next_lat; oc = (float)next_cpu; }
             const int z = em_zone(em[e]);
