@@ -52,6 +52,56 @@ __device__ __forceinline__ void tpe_request_draws(const Params& p, int64_t env, 
     }
 }
 
+// Philox mode: an episode's scenario (endpoint latencies and hosts, node types / zones /
+// cpu, topology) is a pure function of (seed, global env id, episode), so the step
+// recomputes what it needs instead of loading it: 19 Philox blocks replace 112 of the
+// ~220 bytes per env-step it reads (lat0 f64 + emeta per endpoint, topology, node zones).
+// Measured (tools/ablate.py, default scenario): 2^20 envs 0.111 -> 0.107 ms, 2^22 envs
+// 0.678 -> 0.591 ms.  reset() still stores the scenario (lb_get_field / lb_policy read
+// it); trace mode keeps the stored scenario (its values come from the reference's
+// generator).
+#ifdef LB_ABL_STORED_SCEN
+constexpr bool kRecomputeScenario = false;
+#else
+constexpr bool kRecomputeScenario = true;
+#endif
+
+__device__ __forceinline__ uint64_t scen_topo(const Params& p, int64_t env, uint32_t episode) {
+    U4 a = draw(p, env, episode, 0, D_TOPO), b = draw(p, env, episode, 1, D_TOPO);
+    return (uint64_t)(1 + bounded(a.x, 499)) | ((uint64_t)(1 + bounded(a.y, 499)) << 9) |
+           ((uint64_t)(1 + bounded(a.z, 499)) << 18) | ((uint64_t)(1 + bounded(a.w, 499)) << 27) |
+           ((uint64_t)(1 + bounded(b.x, 499)) << 36) | ((uint64_t)(1 + bounded(b.y, 499)) << 45);
+}
+
+// endpoint latencies / packed metadata of the episode (reset() :328, :379-386)
+__device__ __forceinline__ void tpe_scenario(const Params& p, int64_t env, uint32_t episode,
+                                             double (&lat0)[TPE_E], uint32_t (&em)[TPE_E]) {
+    int node[TPE_E];
+#pragma unroll
+    for (int e = 0; e < TPE_E; ++e) {
+        lat0[e] = 0.0;
+        node[e] = 0;
+        if (e < p.E) {
+            U4 w = draw(p, env, episode, (uint32_t)e, D_EP);
+            lat0[e] = 1.0 + 99.0 * u53(w.x, w.y);
+            node[e] = (int)bounded(w.z, 24);
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < TPE_E; ++e) {
+        em[e] = 0u;
+        if (e < p.E) {
+            int owner = e;  // first endpoint hosted on the same node (shares its cpu)
+#pragma unroll
+            for (int e2 = TPE_E - 1; e2 >= 0; --e2)
+                if (e2 < e && node[e2] == node[e]) owner = e2;
+            int ty, zo, cpu;
+            node_draw<false>(p, env, episode, node[e], ty, zo, cpu);
+            em[e] = em_pack(zo, owner, ty, cpu, node[e]);
+        }
+    }
+}
+
 __device__ __forceinline__ void tpe_image_env(uint32_t* me, const TEnv& v, int flag) {
     me[0] = (uint32_t)v.s.rz | ((uint32_t)v.s.thr_idx << 2) | (uint32_t)flag;
     me[1] = __float_as_uint((float)v.dt);
@@ -244,22 +294,33 @@ __global__ __launch_bounds__(BLOCK) void k_step_tpe(Params p) {
     TEnv v;
     double lat0[TPE_E];
     uint32_t em[TPE_E], ed[TPE_E];
+    constexpr bool stored = TRACE || !kRecomputeScenario;
 #pragma unroll
     for (int e = 0; e < TPE_E; ++e) {
         const int64_t i = (int64_t)e * p.B + ev;
-        lat0[e] = e < E ? ld_state(p.lat0 + i) : 0.0;
-        em[e] = e < E ? ld_state(p.emeta + i) : 0u;
+        if constexpr (stored) {
+            lat0[e] = e < E ? ld_state(p.lat0 + i) : 0.0;
+            em[e] = e < E ? ld_state(p.emeta + i) : 0u;
+        }
         ed[e] = e < E ? ld_state(p.edyn + i) : 0u;
     }
     const int a = ld_state(p.actions + ev);
     v.t = ld_state(p.t + ev);
     v.s = sc_unpack(ld_state(p.sc + ev));
-    v.topo = ld_state(p.topo + ev);
     v.zcap = ld_state(p.zcap + ev);
-    v.nz0 = ld_state(p.nzone + ev);
-    v.nz1 = p.NZW > 1 ? ld_state(p.nzone + p.B + ev) : 0;
     v.acc2 = ld_state(p.acc2 + ev);
     v.acc3 = ld_state(p.acc3 + ev);
+    if constexpr (stored) {
+        v.topo = ld_state(p.topo + ev);
+        v.nz0 = ld_state(p.nzone + ev);
+        v.nz1 = p.NZW > 1 ? ld_state(p.nzone + p.B + ev) : 0;
+    } else {
+        const uint32_t episode = (uint32_t)(v.acc3 >> 32);
+        tpe_scenario(p, ev, episode, lat0, em);
+        v.topo = scen_topo(p, ev, episode);
+        v.nz0 = 0;
+        v.nz1 = 0;
+    }
     v.sum_lat = ld_state(p.sum_lat + ev);
     v.sum_cpu = ld_state(p.sum_cpu + ev);
     v.total = ld_state(p.total + ev);
@@ -375,8 +436,14 @@ __global__ __launch_bounds__(BLOCK) void k_step_tpe(Params p) {
         v.dt = departure - arrival;
         v.t = arrival;
         v.s.thr_idx = (r + 6) % 7;  // endpoint_list[r - 1] (:1117)
-        const uint64_t word = n < 32 ? v.nz0 : (n < 64 ? v.nz1 : p.nzone[(int64_t)(n >> 5) * p.B + ev]);
-        v.s.rz = (int)((word >> (2 * (n & 31))) & 3);
+        if constexpr (stored) {
+            const uint64_t word = n < 32 ? v.nz0 : (n < 64 ? v.nz1 : p.nzone[(int64_t)(n >> 5) * p.B + ev]);
+            v.s.rz = (int)((word >> (2 * (n & 31))) & 3);
+        } else {  // the zone of the request's node (:1120-1121), drawn again
+            int ty, zo, cpu;
+            node_draw<false>(p, ev, (uint32_t)(v.acc3 >> 32), n, ty, zo, cpu);
+            v.s.rz = zo;
+        }
     }
     const bool done = live && v.s.step == p.L;  // (:472)
     if (live) {

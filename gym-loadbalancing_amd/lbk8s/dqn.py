@@ -31,7 +31,11 @@ def linear_schedule(start_e: float, end_e: float, duration: float, t: int) -> fl
 
 
 class DeviceReplayBuffer:
-    """SB3 ReplayBuffer semantics (n_envs-major circular storage) with device tensors."""
+    """SB3 ReplayBuffer semantics (n_envs-major circular storage) with device tensors.
+
+    The write position also lives on the device (`pos_t`), so `add_device` is
+    graph-capturable: one captured vector step serves every slot.  The host mirrors it
+    (`pos`, `full`) for the sampling bound."""
 
     def __init__(self, buffer_size, num_envs, obs_shape, device, generator):
         self.n_envs = num_envs
@@ -42,18 +46,31 @@ class DeviceReplayBuffer:
         self.rewards = torch.zeros((self.size, num_envs), device=device)
         self.dones = torch.zeros((self.size, num_envs), device=device)
         self.pos, self.full = 0, False
+        self.pos_t = torch.zeros(1, dtype=torch.long, device=device)
         self.gen = generator
 
-    def add(self, obs, next_obs, actions, rewards, dones):
-        p = self.pos
-        self.obs[p].copy_(obs)
-        self.next_obs[p].copy_(next_obs)
-        self.actions[p].copy_(actions)
-        self.rewards[p].copy_(rewards)
-        self.dones[p].copy_(dones)
+    def add_device(self, obs, next_obs, actions, rewards, dones):
+        """Device part of add(): write slot pos_t, advance pos_t (no host sync)."""
+        i = self.pos_t
+        self.obs.index_copy_(0, i, obs[None])
+        self.next_obs.index_copy_(0, i, next_obs[None])
+        self.actions.index_copy_(0, i, actions.to(torch.long)[None])
+        self.rewards.index_copy_(0, i, rewards[None])
+        self.dones.index_copy_(0, i, dones[None])
+        self.pos_t.add_(1).remainder_(self.size)
+
+    def advance_host(self):
         self.pos += 1
         if self.pos == self.size:
             self.full, self.pos = True, 0
+
+    def add(self, obs, next_obs, actions, rewards, dones):
+        self.add_device(obs, next_obs, actions, rewards, dones)
+        self.advance_host()
+
+    def clear(self):
+        self.pos, self.full = 0, False
+        self.pos_t.zero_()
 
     def sample(self, batch_size):
         upper = self.size if self.full else self.pos
@@ -77,7 +94,9 @@ class DQN_DeepSets:
     def __init__(self, env, seed=1, torch_deterministic=True, num_steps: int = 100, learning_rate=2.5e-4,
                  buffer_size=10000, gamma=0.99, tau=1.0, n_minibatches: int = 4, target_network_frequency=500,
                  batch_size=128, start_e=1, end_e=0.05, exploration_fraction=0.5, learning_starts=10000,
-                 train_frequency=10, device=None, log_fn=None):
+                 train_frequency=10, device=None, log_fn=None, num_envs=None, tensorboard_log=None):
+        # num_envs / tensorboard_log: accepted for signature compatibility with
+        # dqn_deepset.py:46-67 (the env's num_envs is used; there is no tensorboard writer)
         self.env = env
         self.device = torch.device(device) if device is not None else env.device
         self.num_envs = env.num_envs
@@ -106,14 +125,65 @@ class DQN_DeepSets:
         self._ep_sum = torch.zeros((), dtype=torch.float64, device=self.device)
         self._ep_cnt = torch.zeros((), dtype=torch.float64, device=self.device)
         self.train_steps = 0
+        # static buffers of the captured vector step (HIP graphs on a GPU; eager otherwise)
+        self.use_graphs = self.device.type == "cuda"
+        self._graph = None
+        self._q = torch.zeros((self.num_envs, env.observation_space.shape[0]), device=self.device)
+        self._qfrag = fused.frag_buffer(self.device) if self.use_graphs else None
+        self._obs = torch.zeros_like(self._next_obs)
+        self._masks = torch.ones((self.num_envs, env.action_space.n), dtype=torch.bool, device=self.device)
 
     def select_actions(self, obs, masks, epsilon):
         if random.random() < epsilon:  # one draw decides exploration for every env (:127)
-            probs = masks.float()
-            return torch.multinomial(probs, 1, generator=self.gen).squeeze(-1)
+            return self._explore_actions(masks).long()
         with torch.no_grad():
             q = torch.where(masks, fused.q_forward(self.q_network, obs), torch.full((), HUGE_NEG, device=obs.device))
         return torch.argmax(q, dim=1)
+
+    def _explore_actions(self, masks):
+        """np.random.choice(valid_actions) per env (:128-131).  Masks are always all True
+        (:808-821), so this is a uniform action: the env's Philox draw (D_ACT)."""
+        return self.env.policy("random", out=self._act)
+
+    def _vector_step(self, obs, masks, explore):
+        """One vector step on the device: actions, fused env step, episode-return
+        accumulators, replay write, obs <- next obs.  No host sync; graph-capturable."""
+        env = self.env
+        if explore:
+            self._explore_actions(masks)
+        else:
+            with torch.no_grad():
+                if self.use_graphs:
+                    q = fused.q_forward_graphable(self.q_network, obs, self._q, self._qfrag)
+                else:
+                    q = fused.q_forward(self.q_network, obs)
+                q = torch.where(masks, q, torch.full((), HUGE_NEG, device=obs.device))
+                self._act.copy_(torch.argmax(q, dim=1))
+        env.step_device(self._act, obs_out=self._next_obs, reward_out=self._rew, done_out=self._done_u8)
+        dones = self._done_u8.float()
+        # finished-episode returns accumulate on the device (no per-step host sync)
+        self._ep_sum += (env.ep_stats[:, 0] * dones).sum()
+        self._ep_cnt += dones.sum()
+        self.rb.add_device(obs, self._next_obs, self._act, self._rew, dones)
+        obs.copy_(self._next_obs)
+
+    def _build_graphs(self, obs, masks):
+        """Both vector-step variants captured once as HIP graphs: a vector step is ~20
+        small launches, replayed as one graph without the per-launch host cost.  The
+        warm-up steps run on a side stream before capture; the caller resets afterwards."""
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for explore in (False, True):
+                self._vector_step(obs, masks, explore)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        graphs = {}
+        for explore in (False, True):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._vector_step(obs, masks, explore)
+            graphs[explore] = g
+        return graphs
 
     def train_step(self, global_step):
         obs, actions, next_obs, dones, rewards = self.rb.sample(self.batch_size)
@@ -133,20 +203,28 @@ class DQN_DeepSets:
         env = self.env
         start = time.time()
         env.reset()
-        obs = env.obs.clone()
-        masks = env.action_masks()
+        obs, masks = self._obs, self._masks  # fixed buffers: the captured graphs use them
+        obs.copy_(env.obs)
+        graphs = None
+        if self.use_graphs:
+            if self._graph is None:
+                self._graph = self._build_graphs(obs, masks)
+                # the warm-up / capture steps advanced envs, replay and accumulators: restart
+                env.reset()
+                obs.copy_(env.obs)
+                self.rb.clear()
+                self._ep_sum.zero_()
+                self._ep_cnt.zero_()
+            graphs = self._graph
         loss = None
         for global_step in range(total_timesteps):
             eps = linear_schedule(self.start_e, self.end_e, self.exploration_fraction * total_timesteps, global_step)
-            actions = self.select_actions(obs, masks, eps)
-            self._act.copy_(actions)
-            env.step_device(self._act, obs_out=self._next_obs, reward_out=self._rew, done_out=self._done_u8)
-            dones = self._done_u8.float()
-            # finished-episode returns accumulate on the device (no per-step host sync)
-            self._ep_sum += (env.ep_stats[:, 0] * dones).sum()
-            self._ep_cnt += dones.sum()
-            self.rb.add(obs, self._next_obs, actions, self._rew, dones)
-            obs.copy_(self._next_obs)
+            explore = random.random() < eps  # one draw decides exploration for every env (:127)
+            if graphs is not None:
+                graphs[explore].replay()
+            else:
+                self._vector_step(obs, masks, explore)
+            self.rb.advance_host()
             if global_step > self.learning_starts and global_step % self.train_frequency == 0:
                 loss = self.train_step(global_step)
             if global_step % 1000 == 0 or global_step == total_timesteps - 1:

@@ -113,3 +113,24 @@ def q_forward(qnet, x: torch.Tensor, require: bool = False):
     q = torch.empty((B, R), dtype=torch.float32, device=x.device)
     _launch(frag, x, q, None)
     return q
+
+
+def frag_buffer(device):
+    """A fixed weight-image buffer for q_forward_graphable."""
+    return torch.empty(_native.LB_DS_FRAG_FLOATS, dtype=torch.float32, device=device)
+
+
+@torch.no_grad()
+def q_forward_graphable(qnet, x, out, frag):
+    """Q values of a DQNDeepSetAgent into `out`, packing the live parameters into `frag`
+    first: two launches on fixed buffers, so the pair can be captured in a HIP graph and
+    replayed after optimizer steps (Adam updates the parameters in place)."""
+    net = qnet.q_network.net
+    if not _geometry_ok(net, x):
+        raise RuntimeError(f"fused deep-sets forward does not cover input {tuple(x.shape)} on {x.device}")
+    w, keep = _weights_struct(net, None)
+    L = _native.lib()
+    _native.check(L.lb_ds_pack(C.byref(w), frag.data_ptr(), torch.cuda.current_stream(x.device).cuda_stream))
+    del keep
+    _launch(frag, x, out, None)
+    return out

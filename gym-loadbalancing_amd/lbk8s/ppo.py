@@ -72,7 +72,9 @@ class PPO_DeepSets:
                  update_epochs: int = 4, norm_adv: bool = True, clip_coef: float = 0.2,
                  clip_vloss: bool = True, ent_coef: float = 0.01, vf_coef: float = 0.5,
                  max_grad_norm: float = 0.5, target_kl: Optional[float] = None, seed: int = 1,
-                 device=None, log_fn=None):
+                 device=None, log_fn=None, num_envs=None, tensorboard_log=None):
+        # num_envs / tensorboard_log: accepted for signature compatibility with
+        # ppo_deepset.py:53-75 (the env's num_envs is used; there is no tensorboard writer)
         self.env = env
         self.device = torch.device(device) if device is not None else env.device
         self.num_envs = env.num_envs
