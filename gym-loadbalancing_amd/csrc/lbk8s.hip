@@ -180,6 +180,11 @@ struct Geo {
 // 1.00 ms per step, 4096 envs 8.9 vs 20.7 us.  Both shapes give the same EP = W * EPL
 // (the next power of two >= max(E, 16)), so the state layout does not depend on B.
 [[maybe_unused]] constexpr int64_t WIDE_SLICE_MAX_B = 32768;
+#if defined(LB_ABL_SPLIT_RESET) || defined(LB_ABL_SCEN_SPLIT)
+constexpr bool kSplitReset = true;
+#else
+constexpr bool kSplitReset = false;
+#endif
 
 Geo geometry(const lb_config* c, int64_t B = 0) {
     Geo g;
@@ -450,9 +455,23 @@ int lb_step(void* state, const lb_config* cfg, int64_t num_envs, const int32_t* 
         else hipLaunchKernelGGL(k_step_tpe<false>, dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);
         return check_launch();
     }
+    // many-env shape, kSplitReset: finished envs are reset by a second launch masked by
+    // the done flags
+    const bool split = kSplitReset && num_envs >= WIDE_SLICE_MAX_B && cfg->auto_reset && done_out;
     LB_DISPATCH_SLICE(g.W, g.EPL, {
-        if (tr) hipLaunchKernelGGL((k_step_slice<W, EPL, true>), dim3(slice_blocks(num_envs, W)), dim3(BLOCK), 0, s, p);
-        else hipLaunchKernelGGL((k_step_slice<W, EPL, false>), dim3(slice_blocks(num_envs, W)), dim3(BLOCK), 0, s, p);
+        const unsigned nb = slice_blocks(num_envs, W);
+        if (split) {
+            Params q = p;
+            q.reset_mask = done_out;
+            if (tr) hipLaunchKernelGGL((k_step_slice<W, EPL, true, true>), dim3(nb), dim3(BLOCK), 0, s, p);
+            else hipLaunchKernelGGL((k_step_slice<W, EPL, false, true>), dim3(nb), dim3(BLOCK), 0, s, p);
+            if (int r = check_launch()) return r;
+            if (tr) hipLaunchKernelGGL((k_reset_slice<W, EPL, true>), dim3(nb), dim3(BLOCK), 0, s, q);
+            else hipLaunchKernelGGL((k_reset_slice<W, EPL, false>), dim3(nb), dim3(BLOCK), 0, s, q);
+        } else {
+            if (tr) hipLaunchKernelGGL((k_step_slice<W, EPL, true, false>), dim3(nb), dim3(BLOCK), 0, s, p);
+            else hipLaunchKernelGGL((k_step_slice<W, EPL, false, false>), dim3(nb), dim3(BLOCK), 0, s, p);
+        }
     });
     return check_launch();
 }

@@ -240,6 +240,14 @@ __device__ __forceinline__ void node_draw(const Params& p, int64_t env, uint32_t
     }
 }
 
+// the episode's 4x4 topology block from its two D_TOPO blocks (reset() :331-338)
+__device__ __forceinline__ uint64_t scen_topo(const Params& p, int64_t env, uint32_t episode) {
+    U4 a = draw(p, env, episode, 0, D_TOPO), b = draw(p, env, episode, 1, D_TOPO);
+    return (uint64_t)(1 + bounded(a.x, 499)) | ((uint64_t)(1 + bounded(a.y, 499)) << 9) |
+           ((uint64_t)(1 + bounded(a.z, 499)) << 18) | ((uint64_t)(1 + bounded(a.w, 499)) << 27) |
+           ((uint64_t)(1 + bounded(b.x, 499)) << 36) | ((uint64_t)(1 + bounded(b.y, 499)) << 45);
+}
+
 __device__ __forceinline__ double lat_of(const Params& p, double lat0, uint32_t ed) {
     int j = ed_j(ed);
     return j == 0 ? lat0 : p.lat_lut[(j) * LAT_ROWS + (int)lat0];

@@ -16,6 +16,11 @@ namespace lbk {
 #else
 #define LB_SLICE_OCC
 #endif
+#if defined(LB_ABL_SLICE_SCEN) || defined(LB_ABL_SCEN_SPLIT)
+constexpr bool kSliceScenario = true;   // Philox mode: recompute lat0 / emeta / topology
+#else
+constexpr bool kSliceScenario = false;
+#endif
 
 template <int W>
 __device__ __forceinline__ int slice_sum(int v) {
@@ -116,23 +121,67 @@ __device__ __forceinline__ void slice_write_obs(const Params& p, float* out, int
     }
 }
 
+// Philox mode: the lane's endpoints of the episode (reset() :328, :379-386) drawn again
+// instead of loaded (the draws are a pure function of seed, env id and episode)
 template <int W, int EPL>
+__device__ __forceinline__ void slice_scenario(const Params& p, int64_t env, int lane, uint32_t episode,
+                                               SEnv<EPL>& v) {
+    int node[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+        const int e = lane + k * W;
+        node[k] = 0;
+        v.lat0[k] = 0.0;
+        if (e < p.E) {
+            U4 w = draw(p, env, episode, (uint32_t)e, D_EP);
+            v.lat0[k] = 1.0 + 99.0 * u53(w.x, w.y);
+            node[k] = (int)bounded(w.z, 24);
+        }
+    }
+    int owner[EPL];  // first endpoint hosted on the same node (shares its cpu)
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) owner[k] = lane + k * W;
+    for (int e2 = 0; e2 < p.E; ++e2) {
+        const int nd2 = shfl_u32<W>((uint32_t)sel<EPL>(node, e2 / W), e2 % W);
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) owner[k] = (nd2 == node[k] && e2 < owner[k]) ? e2 : owner[k];
+    }
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+        const int e = lane + k * W;
+        int ty = 0, zo = 0, cpu = 0;
+        if (e < p.E) node_draw<false>(p, env, episode, node[k], ty, zo, cpu);
+        v.em[k] = e < p.E ? em_pack(zo, owner[k], ty, cpu, node[k]) : 0u;
+    }
+}
+
+template <int W, int EPL, bool STORED = true>
 __device__ __forceinline__ void slice_load(const Params& p, int64_t env, int lane, SEnv<EPL>& v) {
 #pragma unroll
     for (int k = 0; k < EPL; ++k) {
         int64_t i = eidx(p, env, lane + k * W);
-        v.lat0[k] = p.lat0[i];
-        v.em[k] = p.emeta[i];
+        if constexpr (STORED) {
+            v.lat0[k] = p.lat0[i];
+            v.em[k] = p.emeta[i];
+        }
         v.ed[k] = p.edyn[i];
     }
     v.t = p.t[env];
     v.s = sc_unpack(p.sc[env]);
-    v.topo = p.topo[env];
     v.zcap = p.zcap[env];
-    v.nz0 = p.nzone[env];
-    v.nz1 = p.NZW > 1 ? p.nzone[p.B + env] : 0;
     v.acc2 = p.acc2[env];
     v.acc3 = p.acc3[env];
+    if constexpr (STORED) {
+        v.topo = p.topo[env];
+        v.nz0 = p.nzone[env];
+        v.nz1 = p.NZW > 1 ? p.nzone[p.B + env] : 0;
+    } else {
+        const uint32_t episode = (uint32_t)(v.acc3 >> 32);
+        slice_scenario<W, EPL>(p, env, lane, episode, v);
+        v.topo = scen_topo(p, env, episode);
+        v.nz0 = 0;
+        v.nz1 = 0;
+    }
     v.sum_lat = p.sum_lat[env];
     v.sum_cpu = p.sum_cpu[env];
     v.total = p.total[env];
@@ -152,7 +201,7 @@ __device__ __forceinline__ void slice_store_scalars(const Params& p, int64_t env
 }
 
 // the request part of next_request() (:1131-1163); the dequeue part is folded into the LUTs
-template <int W, bool TRACE, int EPL>
+template <int W, bool TRACE, int EPL, bool DRAW_ZONE = false>
 __device__ __forceinline__ void slice_next_request(const Params& p, int64_t env, int lane, bool from_reset,
                                                    SEnv<EPL>& v) {
     double x1, x2;
@@ -164,8 +213,14 @@ __device__ __forceinline__ void slice_next_request(const Params& p, int64_t env,
     v.dt = departure - arrival;
     v.t = arrival;
     v.s.thr_idx = (r + 6) % 7;  // endpoint_list[r - 1] (:1117)
-    uint64_t word = n < 32 ? v.nz0 : (n < 64 ? v.nz1 : p.nzone[(n >> 5) * p.B + env]);
-    v.s.rz = (int)((word >> (2 * (n & 31))) & 3);
+    if constexpr (DRAW_ZONE) {  // the zone of the request's node (:1120-1121), drawn again
+        int ty, zo, cpu;
+        node_draw<false>(p, env, (uint32_t)(v.acc3 >> 32), n, ty, zo, cpu);
+        v.s.rz = zo;
+    } else {
+        uint64_t word = n < 32 ? v.nz0 : (n < 64 ? v.nz1 : p.nzone[(n >> 5) * p.B + env]);
+        v.s.rz = (int)((word >> (2 * (n & 31))) & 3);
+    }
 }
 
 // reset() (:290-400) into registers, then the per-episode state stores.
@@ -283,15 +338,18 @@ __global__ __launch_bounds__(BLOCK) void k_reset_slice(Params p) {
 }
 
 // step() (:403-513) fused with next_request(), get_state(), reward, done and auto-reset.
-template <int W, int EPL, bool TRACE>
+// SPLIT: the reset of envs that finish is left to a k_reset_slice launch masked by the
+// done flags, so reset()'s draws do not raise this kernel's register count.
+template <int W, int EPL, bool TRACE, bool SPLIT>
 __global__ __launch_bounds__(BLOCK) LB_SLICE_OCC void k_step_slice(Params p) {
+    constexpr bool stored = TRACE || !kSliceScenario;
     const int lane = threadIdx.x % W;
     const int64_t env = (int64_t)blockIdx.x * (BLOCK / W) + threadIdx.x / W;
     if (env >= p.B) return;
     const int E = p.E;
     // ---- phase 0: independent loads (state + action)
     SEnv<EPL> v;
-    slice_load<W, EPL>(p, env, lane, v);
+    slice_load<W, EPL, stored>(p, env, lane, v);
     const int a = p.actions[env];
 
     // ---- phase 1: decode, then every table lookup the step needs, issued together
@@ -382,7 +440,7 @@ __global__ __launch_bounds__(BLOCK) LB_SLICE_OCC void k_step_slice(Params p) {
     v.total += reward;
 
     // ---- next_request (:1131-1163), done (:472), outputs
-    slice_next_request<W, TRACE, EPL>(p, env, lane, false, v);
+    slice_next_request<W, TRACE, EPL, !stored>(p, env, lane, false, v);
     const bool done = v.s.step == p.L;
     if (lane == 0) {
         if (p.reward) p.reward[env] = (float)reward;
@@ -392,7 +450,7 @@ __global__ __launch_bounds__(BLOCK) LB_SLICE_OCC void k_step_slice(Params p) {
         if (p.term_obs) slice_write_obs<W, EPL>(p, p.term_obs, env, lane, v);
         if (p.ep_stats && lane == 0)
             write_stats_row(p, p.ep_stats + env * LB_ST_K, v.s, v.acc2, v.acc3, v.total, v.sum_lat, v.sum_cpu);
-        slice_reset<W, EPL, TRACE>(p, env, lane, v);
+        if constexpr (!SPLIT) slice_reset<W, EPL, TRACE>(p, env, lane, v);
     } else if (accept) {
 #pragma unroll
         for (int k = 0; k < EPL; ++k) {
@@ -400,7 +458,7 @@ __global__ __launch_bounds__(BLOCK) LB_SLICE_OCC void k_step_slice(Params p) {
             if (e == ai || e == oA) p.edyn[eidx(p, env, e)] = v.ed[k];
         }
     }
-    if (p.obs) slice_write_obs<W, EPL>(p, p.obs, env, lane, v);
+    if (p.obs && !(SPLIT && done && p.auto_reset)) slice_write_obs<W, EPL>(p, p.obs, env, lane, v);
     if (lane == 0) slice_store_scalars<EPL>(p, env, v);
 }
 

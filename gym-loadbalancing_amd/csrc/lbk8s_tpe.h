@@ -66,13 +66,6 @@ constexpr bool kRecomputeScenario = false;
 constexpr bool kRecomputeScenario = true;
 #endif
 
-__device__ __forceinline__ uint64_t scen_topo(const Params& p, int64_t env, uint32_t episode) {
-    U4 a = draw(p, env, episode, 0, D_TOPO), b = draw(p, env, episode, 1, D_TOPO);
-    return (uint64_t)(1 + bounded(a.x, 499)) | ((uint64_t)(1 + bounded(a.y, 499)) << 9) |
-           ((uint64_t)(1 + bounded(a.z, 499)) << 18) | ((uint64_t)(1 + bounded(a.w, 499)) << 27) |
-           ((uint64_t)(1 + bounded(b.x, 499)) << 36) | ((uint64_t)(1 + bounded(b.y, 499)) << 45);
-}
-
 // endpoint latencies / packed metadata of the episode (reset() :328, :379-386)
 __device__ __forceinline__ void tpe_scenario(const Params& p, int64_t env, uint32_t episode,
                                              double (&lat0)[TPE_E], uint32_t (&em)[TPE_E]) {
