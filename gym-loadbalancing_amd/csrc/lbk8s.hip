@@ -451,8 +451,10 @@ int lb_step(void* state, const lb_config* cfg, int64_t num_envs, const int32_t* 
     Geo g = geometry(cfg, num_envs);
     hipStream_t s = (hipStream_t)stream;
     if (g.tpe) {
-        if (tr) hipLaunchKernelGGL(k_step_tpe<true>, dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);
-        else hipLaunchKernelGGL(k_step_tpe<false>, dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);
+        const bool recompute = kRecomputeScenario && num_envs >= SCEN_RECOMPUTE_MIN_B;
+        if (tr) hipLaunchKernelGGL((k_step_tpe<true, false>), dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);
+        else if (recompute) hipLaunchKernelGGL((k_step_tpe<false, true>), dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);
+        else hipLaunchKernelGGL((k_step_tpe<false, false>), dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);
         return check_launch();
     }
     // many-env shape, kSplitReset: finished envs are reset by a second launch masked by

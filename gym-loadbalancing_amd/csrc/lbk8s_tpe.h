@@ -57,14 +57,17 @@ __device__ __forceinline__ void tpe_request_draws(const Params& p, int64_t env, 
 // recomputes what it needs instead of loading it: 19 Philox blocks replace 112 of the
 // ~220 bytes per env-step it reads (lat0 f64 + emeta per endpoint, topology, node zones).
 // Measured (tools/ablate.py, default scenario): 2^20 envs 0.111 -> 0.107 ms, 2^22 envs
-// 0.678 -> 0.591 ms.  reset() still stores the scenario (lb_get_field / lb_policy read
-// it); trace mode keeps the stored scenario (its values come from the reference's
-// generator).
+// 0.678 -> 0.591 ms; but below 2^18 envs, where a step is latency bound rather than
+// bandwidth bound, the serial Philox work lengthens each wave (4096 envs 12.6 -> 15.0 us),
+// so lb_step recomputes only from SCEN_RECOMPUTE_MIN_B envs.  reset() still stores the
+// scenario (lb_get_field / lb_policy read it); trace mode keeps the stored scenario (its
+// values come from the reference's generator).
 #ifdef LB_ABL_STORED_SCEN
 constexpr bool kRecomputeScenario = false;
 #else
 constexpr bool kRecomputeScenario = true;
 #endif
+constexpr int64_t SCEN_RECOMPUTE_MIN_B = 1 << 18;
 
 // endpoint latencies / packed metadata of the episode (reset() :328, :379-386)
 __device__ __forceinline__ void tpe_scenario(const Params& p, int64_t env, uint32_t episode,
@@ -271,7 +274,8 @@ __global__ __launch_bounds__(BLOCK) void k_reset_tpe(Params p) {
 }
 
 // step() (:403-513) fused with next_request(), get_state(), reward, done and auto-reset.
-template <bool TRACE>
+// RECOMPUTE (Philox mode, many envs): the scenario is redrawn instead of loaded.
+template <bool TRACE, bool RECOMPUTE>
 __global__ __launch_bounds__(BLOCK) void k_step_tpe(Params p) {
     __shared__ uint32_t lds[BLOCK * TPE_CW];
     const int lane = threadIdx.x & 63;
@@ -287,7 +291,7 @@ __global__ __launch_bounds__(BLOCK) void k_step_tpe(Params p) {
     TEnv v;
     double lat0[TPE_E];
     uint32_t em[TPE_E], ed[TPE_E];
-    constexpr bool stored = TRACE || !kRecomputeScenario;
+    constexpr bool stored = TRACE || !RECOMPUTE;
 #pragma unroll
     for (int e = 0; e < TPE_E; ++e) {
         const int64_t i = (int64_t)e * p.B + ev;

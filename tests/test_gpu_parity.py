@@ -118,14 +118,20 @@ def test_philox_mode_matches_oracle(oracle_mod, name):
     assert env.status() & 1
 
 
-# Many envs (B >= 32768, E > 8) take the 4-envs-per-wave slice shape (W = 16 or 32 lanes
-# per env, 2 or 4 endpoints per lane); fewer envs take one env per wave.  Same check as
-# above at a size that selects the many-env shape, with short episodes so auto-resets run.
+# Many envs take other kernel variants: from 32,768 envs (E > 8) the 4-envs-per-wave
+# slice shape (W = 16 or 32 lanes per env, 2 or 4 endpoints per lane), from 262,144 envs
+# (E <= 8) the thread-per-env step that redraws the scenario instead of loading it.  Same
+# check as above at sizes that select them, with short episodes so auto-resets run.
 MANY_CFGS = {
     "e64_multi_l10": dict(num_endpoints=64, reward_function="multi", episode_length=10),
     "e20_latency_l10": dict(num_endpoints=20, reward_function="latency", episode_length=10),
     "e100_fair_norej_l10": dict(num_endpoints=100, reward_function="fairness", rejection_allowed=False,
                                 episode_length=10),
+    "default_l10": dict(episode_length=10),
+    "cfg1_multi_l7": dict(num_endpoints=6, num_nodes=48, num_zones=12, reward_function="multi",
+                          latency_weight=0.5, cpu_weight=0.3, gini_weight=0.2, episode_length=7),
+    "e5_fair_norej_l10": dict(num_endpoints=5, num_nodes=70, reward_function="fairness",
+                              rejection_allowed=False, episode_length=10),
 }
 
 
@@ -133,7 +139,7 @@ MANY_CFGS = {
 def test_philox_many_envs_matches_oracle(oracle_mod, name):
     from lbk8s import LBVecEnv
     cfg = MANY_CFGS[name]
-    B = 32768
+    B = 32768 if cfg.get("num_endpoints", 8) > 8 else 262144
     seed = 99
     env = LBVecEnv(B, seed=seed, **cfg)
     orc = oracle_mod.OracleBatch(cfg, B, trace=False, seed=seed)

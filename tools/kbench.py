@@ -2,7 +2,13 @@
 """Kernel micro-bench: lb_step time vs batch size and scenario (one process, HIP events).
 
     python tools/kbench.py [--configs default,cfg1,e64_multi] [--sizes 16,18,20,22]
+    python tools/kbench.py --config2          # BASELINE config 2: 4096 envs, random policy
 Prints one JSON line per (config, B): ms per step, env-steps/s, algorithmic GB/s.
+
+--config2: 4096 default envs driven by the env's own Philox random policy (lb_policy +
+lb_step per vector step), 1,000 warm-up + 10,000 timed vector steps, launched eagerly and
+as HIP graphs of 100 vector steps each (at this size a step is a few microseconds of GPU
+time, below the cost of launching it from the host).
 """
 import argparse
 import json
@@ -21,11 +27,14 @@ def main():
     ap.add_argument("--sizes", default="16,18,20,22")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--ring", type=int, default=16)
+    ap.add_argument("--config2", action="store_true")
     args = ap.parse_args()
     import torch
 
     from lbk8s import LBVecEnv
     dev = torch.device("cuda", 0)
+    if args.config2:
+        return config2(torch, LBVecEnv, dev)
     for name in args.configs.split(","):
         for lg in (int(x) for x in args.sizes.split(",")):
             B = 1 << lg
@@ -55,6 +64,43 @@ def main():
                                   bytes_per_env_step=b)), flush=True)
             del env, ring, rew, dn, acts
             torch.cuda.empty_cache()
+
+
+def config2(torch, LBVecEnv, dev, B=4096, warmup=1000, steps=10000, per_graph=100):
+    env = LBVecEnv(B, device=dev, seed=0, as_tensors=True)
+    R, T = env.cfg.obs_rows, 100
+    ring = torch.empty((T, B, R, 8), dtype=torch.float32, device=dev)
+    rew = torch.empty((T, B), dtype=torch.float32, device=dev)
+    dn = torch.empty((T, B), dtype=torch.uint8, device=dev)
+    act = torch.empty(B, dtype=torch.int32, device=dev)
+    env.reset()
+
+    def vector_step(i):
+        env.policy("random", out=act)
+        env.step_device(act, obs_out=ring[i % T], reward_out=rew[i % T], done_out=dn[i % T])
+
+    def timed(fn, n):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s.record()
+        fn(n)
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e)
+
+    for i in range(warmup):
+        vector_step(i)
+    eager_ms = timed(lambda n: [vector_step(i) for i in range(n)], steps)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for i in range(per_graph):
+            vector_step(i)
+    g.replay()
+    graph_ms = timed(lambda n: [g.replay() for _ in range(n // per_graph)], steps)
+    assert env.status() == 0
+    for mode, ms in (("eager", eager_ms), ("hip_graph", graph_ms)):
+        print(json.dumps(dict(config="config2 default, random policy", envs=B, mode=mode, vector_steps=steps,
+                              ms_per_step=round(ms / steps, 5), env_steps_per_s=B * steps / ms * 1e3)), flush=True)
 
 
 if __name__ == "__main__":
