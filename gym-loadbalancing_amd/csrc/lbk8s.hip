@@ -22,6 +22,7 @@
 #include "lbk8s.h"
 #include "lbk8s_common.h"
 #include "lbk8s_deepsets.h"
+#include "lbk8s_ds_train.h"
 #include "lbk8s_slice.h"
 #include "lbk8s_tpe.h"
 
@@ -526,6 +527,33 @@ int lb_ds_pack(const lb_ds_weights* w, float* frag_out, void* stream) {
     return check_launch();
 }
 
+}  // extern "C"
+
+namespace {
+// persistent grid for the deep-sets kernels (the weight image is staged once per block)
+unsigned ds_grid(int64_t groups) {
+    const int64_t want = (groups + DS_BLOCK / 64 - 1) / (DS_BLOCK / 64);
+    return (unsigned)std::min<int64_t>(want, device_cus());
+}
+
+template <bool TRAIN>
+void ds_forward_launch(const DSParams& p, hipStream_t s) {
+    // a wave takes P envs per iteration: P = 4 for R <= 16, 2 for R <= 32, else 1
+    const int ts = (p.R + 15) / 16;
+    const int P = ts == 1 ? 4 : (ts == 2 ? 2 : 1);
+    const unsigned grid = ds_grid((p.B + P - 1) / P);
+    switch (ts) {
+        case 1: hipLaunchKernelGGL((k_deepsets_fwd<1, 4, TRAIN>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        case 2: hipLaunchKernelGGL((k_deepsets_fwd<2, 2, TRAIN>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        case 3: hipLaunchKernelGGL((k_deepsets_fwd<3, 1, TRAIN>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        case 4: hipLaunchKernelGGL((k_deepsets_fwd<4, 1, TRAIN>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        default: hipLaunchKernelGGL((k_deepsets_fwd<5, 1, TRAIN>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+    }
+}
+}  // namespace
+
+extern "C" {
+
 int lb_ds_forward(const float* frag, const float* obs, int64_t num_envs, int32_t num_elements, float* logits_out,
                   float* value_out, void* stream) {
     static_assert(DS_FLOATS == LB_DS_FRAG_FLOATS, "fragment layout and header disagree");
@@ -533,21 +561,56 @@ int lb_ds_forward(const float* frag, const float* obs, int64_t num_envs, int32_t
     if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS)
         return fail("num_elements must be in [1, 80] (LB_DS_MAX_ELEMENTS)");
     if (!logits_out && !value_out) return 0;
-    DSParams p{obs, frag, logits_out, value_out, num_envs, num_elements, logits_out != nullptr, value_out != nullptr};
-    // persistent blocks (the 132 KiB weight image is staged once per block); a wave takes
-    // P envs per iteration: P = 4 for R <= 16, 2 for R <= 32, else 1
-    const int ts = (num_elements + 15) / 16;
-    const int P = ts == 1 ? 4 : (ts == 2 ? 2 : 1);
-    const int64_t groups = (num_envs + P - 1) / P;
-    const int64_t want = (groups + DS_BLOCK / 64 - 1) / (DS_BLOCK / 64);
-    const unsigned grid = (unsigned)std::min<int64_t>(want, device_cus());
+    DSParams p{obs, frag, logits_out, value_out, num_envs, num_elements, logits_out != nullptr, value_out != nullptr,
+               nullptr, nullptr, nullptr};
+    ds_forward_launch<false>(p, (hipStream_t)stream);
+    return check_launch();
+}
+
+int lb_ds_train_forward(const float* frag, const float* obs, int64_t num_envs, int32_t num_elements,
+                        float* logits_out, float* psi_mean_out, float* save_actor, float* save_critic, void* stream) {
+    if (!frag || !obs || num_envs < 1) return fail("frag/obs NULL or num_envs < 1");
+    if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS)
+        return fail("num_elements must be in [1, 80] (LB_DS_MAX_ELEMENTS)");
+    if (!logits_out && !psi_mean_out) return 0;
+    if ((logits_out && !save_actor) || (psi_mean_out && !save_critic))
+        return fail("a head's activation buffer is NULL");
+    DSParams p{obs, frag, logits_out, nullptr, num_envs, num_elements, logits_out != nullptr, psi_mean_out != nullptr,
+               save_actor, save_critic, psi_mean_out};
+    ds_forward_launch<true>(p, (hipStream_t)stream);
+    return check_launch();
+}
+
+int lb_ds_pack_backward(const lb_ds_weights* w, float* bwd_frag_out, void* stream) {
+    static_assert(DSB_FLOATS == LB_DS_BWD_FLOATS, "backward image layout and header disagree");
+    if (!w || !bwd_frag_out) return fail("weights/bwd_frag_out NULL");
+    if (!w->actor_lambda[1] || !w->actor_gamma[1] || !w->actor_lambda[2] || !w->actor_gamma[2])
+        return fail("actor weights are required");
+    hipLaunchKernelGGL(k_ds_pack_bwd, dim3((DSB_FLOATS + 255) / 256), dim3(256), 0, (hipStream_t)stream, *w,
+                       bwd_frag_out);
+    return check_launch();
+}
+
+int lb_ds_train_backward(const float* bwd_frag, const float* obs, int64_t num_envs, int32_t num_elements,
+                         const float* save_actor, const float* save_critic, const float* dlogits, const float* dmean,
+                         float* gz_actor, float* gz_critic, float* setvec, void* stream) {
+    static_assert(DSV_FLOATS == LB_DS_SETVEC_FLOATS, "per-set vector layout and header disagree");
+    if (!bwd_frag || !obs || !setvec || num_envs < 1) return fail("bwd_frag/obs/setvec NULL or num_envs < 1");
+    if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS)
+        return fail("num_elements must be in [1, 80] (LB_DS_MAX_ELEMENTS)");
+    const bool actor = dlogits != nullptr, critic = dmean != nullptr;
+    if ((actor && (!save_actor || !gz_actor)) || (critic && (!save_critic || !gz_critic)))
+        return fail("a head's activation / gradient buffer is NULL");
+    DSBwdParams p{obs, bwd_frag, save_actor, save_critic, dlogits, dmean, gz_actor, gz_critic, setvec,
+                  num_envs, num_elements, actor, critic};
+    const unsigned grid = ds_grid(num_envs);
     hipStream_t s = (hipStream_t)stream;
-    switch (ts) {
-        case 1: hipLaunchKernelGGL((k_deepsets_fwd<1, 4>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
-        case 2: hipLaunchKernelGGL((k_deepsets_fwd<2, 2>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
-        case 3: hipLaunchKernelGGL((k_deepsets_fwd<3, 1>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
-        case 4: hipLaunchKernelGGL((k_deepsets_fwd<4, 1>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
-        default: hipLaunchKernelGGL((k_deepsets_fwd<5, 1>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+    switch ((num_elements + 15) / 16) {
+        case 1: hipLaunchKernelGGL((k_ds_train_bwd<1>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        case 2: hipLaunchKernelGGL((k_ds_train_bwd<2>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        case 3: hipLaunchKernelGGL((k_ds_train_bwd<3>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        case 4: hipLaunchKernelGGL((k_ds_train_bwd<4>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        default: hipLaunchKernelGGL((k_ds_train_bwd<5>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
     }
     return check_launch();
 }

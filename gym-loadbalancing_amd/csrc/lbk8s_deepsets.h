@@ -36,6 +36,10 @@ struct DSParams {
     int64_t B;
     int R;
     int actor, critic;    // which heads to evaluate (DQN: actor only)
+    // training forward (TRAIN = true) only: activations kept for lb_ds_train_backward
+    float* save_actor;    // [2][B][R][64]: actor h1 (after ReLU), h2 (after ELU)
+    float* save_critic;   // [2][B][R][64]: critic c1, c2 (after ELU)
+    float* psi_mean;      // [B][64]: critic psi output averaged over the set (rho runs in torch)
 };
 
 // fragment layout of the packed weights (floats).  A matrix with KS input k-steps and NT
@@ -174,7 +178,26 @@ __device__ __forceinline__ void eq_layer(const float* L, const float* G, const f
     }
 }
 
+// store a layer output (accumulator layout) row-major into plane [B][R][64]
 template <int TS, int P>
+__device__ __forceinline__ void store_rows(float* plane, const float (&h)[P * TS][16], int64_t env0, int64_t B,
+                                           int R, int col, int grp) {
+#pragma unroll
+    for (int s = 0; s < P; ++s)
+#pragma unroll
+        for (int t = 0; t < TS; ++t) {
+            const int row = 16 * t + col;
+            if (env0 + s >= B || row >= R) continue;
+            float* q = plane + ((env0 + s) * (int64_t)R + row) * 64 + 4 * grp;
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt)
+                *reinterpret_cast<float4*>(q + 16 * nt) =
+                    make_float4(h[s * TS + t][4 * nt], h[s * TS + t][4 * nt + 1], h[s * TS + t][4 * nt + 2],
+                                h[s * TS + t][4 * nt + 3]);
+        }
+}
+
+template <int TS, int P, bool TRAIN>
 __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
     __shared__ __attribute__((aligned(16))) float W[DS_LDS_FLOATS];
     // stage the weight fragments (once per block; blocks are persistent)
@@ -209,8 +232,10 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
         // ---- actor: Eq(8->64) ReLU Eq(64->64) ELU Eq(64->1)
         if (p.actor) {
             eq_layer<TS, P, 2, 1>(W + DS_A1L, W + DS_A1G, h0, m0, h1, lane);
+            if (TRAIN) store_rows<TS, P>(p.save_actor, h1, env0, p.B, R, col, grp);
             set_max_batched<TS, P, 16>(h1, m1, col, R);
             eq_layer<TS, P, 16, 2>(W + DS_A2L, W + DS_A2G, h1, m1, h2, lane);
+            if (TRAIN) store_rows<TS, P>(p.save_actor + p.B * (int64_t)R * 64, h2, env0, p.B, R, col, grp);
             set_max_batched<TS, P, 16>(h2, m2, col, R);
             const float* L = W + DS_A3L;
             const float* G = W + DS_A3G;
@@ -234,8 +259,10 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
 
         // ---- critic: psi = Eq ELU Eq ELU Eq, mean over the set, rho = Linear ELU Linear
         eq_layer<TS, P, 2, 2>(W + DS_C1L, W + DS_C1G, h0, m0, h1, lane);
+        if (TRAIN) store_rows<TS, P>(p.save_critic, h1, env0, p.B, R, col, grp);
         set_max_batched<TS, P, 16>(h1, m1, col, R);
         eq_layer<TS, P, 16, 2>(W + DS_C2L, W + DS_C2G, h1, m1, h2, lane);
+        if (TRAIN) store_rows<TS, P>(p.save_critic + p.B * (int64_t)R * 64, h2, env0, p.B, R, col, grp);
         set_max_batched<TS, P, 16>(h2, m2, col, R);
         eq_layer<TS, P, 16, 0>(W + DS_C3L, W + DS_C3G, h2, m2, h1, lane);
         // batched mean: column c carries env (c mod P)'s mean over its valid set elements
@@ -261,6 +288,17 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
                 for (int s = 1; s < P; ++s) r = (col % P == s) ? sm[k * P + s] : r;
                 mean[k] = r * invR;
             }
+        }
+        if (TRAIN) {
+            // column c carries env (c mod P): lanes of columns < P store their env's features
+            if (col < P && env0 + col < p.B) {
+                float* q = p.psi_mean + (env0 + col) * 64 + 4 * grp;
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt)
+                    *reinterpret_cast<float4*>(q + 16 * nt) =
+                        make_float4(mean[4 * nt], mean[4 * nt + 1], mean[4 * nt + 2], mean[4 * nt + 3]);
+            }
+            continue;
         }
         float r1[16];
 #pragma unroll

@@ -1,0 +1,346 @@
+// lbk8s_ds_train.h — fused deep-sets backward for the PPO / DQN updates on MI355X.
+//
+// Reference: the update's autograd through envs/deep_sets_agent_original.py:56-106
+// (EquivariantLayer y = Lambda(x) - Gamma(max_set x), the actor Eq-ReLU-Eq-ELU-Eq and the
+// critic Eq-ELU-Eq-ELU-Eq-mean), as driven by envs/ppo_deepset.py:227-263.
+//
+// Split of the training step:
+//   * k_deepsets_fwd<TS, P, true> (lbk8s_deepsets.h) writes the logits, the critic's psi
+//     mean and the hidden activations h1, h2 (actor) / c1, c2 (critic) row-major.
+//   * torch evaluates rho, the PPO loss and its gradient w.r.t. logits and psi mean.
+//   * k_ds_train_bwd (here), one wave per set: back through every equivariant layer in
+//     registers — the set-wise max's argmax is recomputed from the saved activation, the
+//     activation derivative is taken from the activation itself (ReLU: y > 0; ELU: y > 0 ?
+//     1 : y + 1), the data gradient of each 64x64 layer is an f32 MFMA against the
+//     transposed Lambda — and writes what the weight gradients need: the layer-2 and
+//     layer-1 pre-activation gradients (row-major, for split-K GEMMs against h1 / obs) and
+//     per-set vectors (set-wise max, gradient sums over the set, the actor's last-layer
+//     and the critic's last-layer products), from which every Gamma gradient and the
+//     rank-1 last-layer gradients are small GEMMs over the sets.
+// Layout conventions (fragment order, accumulator layout) are those of lbk8s_deepsets.h:
+// lane l holds set element (l & 15) of each 16-row tile, and at k-step k the features
+// 16(k >> 2) + 4(l >> 4) + (k & 3).
+#pragma once
+
+#include "lbk8s_deepsets.h"
+
+namespace lbk {
+
+// backward weight image: transposed 64x64 matrices in fragment order, then the actor's
+// last-layer rows in natural order
+enum : int {
+    DSB_A2LT = 0, DSB_A2GT = 4096, DSB_C2LT = 8192, DSB_C2GT = 12288, DSB_C3LT = 16384, DSB_C3GT = 20480,
+    DSB_A3L = 24576, DSB_A3G = 24640, DSB_FLOATS = 24704,
+};
+// per-set vector block (floats); every 64-wide entry is indexed by input feature
+enum : int {
+    DSV_MAX0 = 0,     // [8]  max over the set of the observation
+    DSV_GA3 = 8,      // actor: sum_r dlogit[r] h2[r]           (Lambda3 gradient)
+    DSV_MAX2A = 72,   //        max_set h2                       (Gamma3)
+    DSV_GS2A = 136,   //        sum_r dz2[r]                     (Gamma2)
+    DSV_MAX1A = 200,  //        max_set h1                       (Gamma2)
+    DSV_GS1A = 264,   //        sum_r dz1[r]                     (Gamma1)
+    DSV_CS2 = 328,    // critic: sum_r c2[r]                     (Lambda3: rank 1, d psi = dmean / R)
+    DSV_MAX2C = 392,  //         max_set c2                      (Gamma3)
+    DSV_GS2C = 456,   //         sum_r dz2[r]
+    DSV_MAX1C = 520,  //         max_set c1
+    DSV_GS1C = 584,   //         sum_r dz1[r]
+    DSV_FLOATS = 648,
+};
+
+struct DSBwdParams {
+    const float* obs;          // [B][R][8]
+    const float* wb;           // backward weight image [DSB_FLOATS]
+    const float* save_actor;   // [2][B][R][64] h1, h2
+    const float* save_critic;  // [2][B][R][64] c1, c2
+    const float* dlogits;      // [B][R]
+    const float* dmean;        // [B][64]
+    float* gz_actor;           // [2][B][R][64] dz2, dz1 (pre-activation gradients)
+    float* gz_critic;          // [2][B][R][64]
+    float* setvec;             // [B][DSV_FLOATS]
+    int64_t B;
+    int R;
+    int actor, critic;
+};
+
+template <int TS>
+__device__ __forceinline__ void load_rows(const float* plane, float (&h)[TS][16], int64_t env, int R, int col,
+                                          int grp) {
+#pragma unroll
+    for (int t = 0; t < TS; ++t) {
+        const int row = 16 * t + col;
+        if (row < R) {
+            const float* q = plane + (env * (int64_t)R + row) * 64 + 4 * grp;
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                const float4 v = *reinterpret_cast<const float4*>(q + 16 * nt);
+                h[t][4 * nt] = v.x;
+                h[t][4 * nt + 1] = v.y;
+                h[t][4 * nt + 2] = v.z;
+                h[t][4 * nt + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) h[t][k] = 0.f;
+        }
+    }
+}
+
+// a 16-feature vector in k layout (every lane of a row holds it): column-0 lanes store it
+__device__ __forceinline__ void store_vec(float* dst, const float (&v)[16], int col, int grp) {
+    if (col != 0) return;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+        *reinterpret_cast<float4*>(dst + 16 * nt + 4 * grp) = make_float4(v[4 * nt], v[4 * nt + 1], v[4 * nt + 2], v[4 * nt + 3]);
+}
+
+// per feature: max over the set's valid rows and the FIRST row attaining it (torch.max's
+// index, where the reference's autograd sends the pooled gradient)
+template <int TS>
+__device__ __forceinline__ void set_max_idx(const float (&h)[TS][16], float (&mx)[16], int (&id)[16], int col, int R) {
+    float m[16], c[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        float v = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < TS; ++t)
+            if (16 * t + col < R) v = max2(v, h[t][k]);
+        m[k] = v;
+    }
+    row_reduce<true>(m);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        float v = -1e9f;  // max of -row == min row
+#pragma unroll
+        for (int t = 0; t < TS; ++t) {
+            const int row = 16 * t + col;
+            if (row < R && h[t][k] == m[k]) v = max2(v, -(float)row);
+        }
+        c[k] = v;
+    }
+    row_reduce<true>(c);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        mx[k] = m[k];
+        id[k] = (int)(-c[k]);
+    }
+}
+
+// sum over the set (rows past R hold 0)
+template <int TS>
+__device__ __forceinline__ void set_sum(const float (&h)[TS][16], float (&s)[16]) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        float v = 0.f;
+#pragma unroll
+        for (int t = 0; t < TS; ++t) v += h[t][k];
+        s[k] = v;
+    }
+    row_reduce<false>(s);
+}
+
+// d act / d z from the activation's output: ReLU (ACT 1) y > 0; ELU (ACT 2) y > 0 ? 1 : y + 1
+template <int ACT>
+__device__ __forceinline__ float dact(float y) {
+    return ACT == 1 ? (y > 0.f ? 1.f : 0.f) : (y > 0.f ? 1.f : y + 1.f);
+}
+
+// Back through a 64 -> 64 equivariant layer z = Lambda h - Gamma max_set(h), h = act(z_prev):
+// g = dz (this layer), gs = sum_r dz; h (in: the layer input, out: dz of the layer below)
+//   dh[r][i] = sum_o Lambda[o][i] dz[r][o] - [r == argmax_i] sum_o Gamma[o][i] gs[o]
+//   dz_prev  = dh * act'(h)
+template <int TS, int ACT>
+__device__ __forceinline__ void eq_back64(const float* LT, const float* GT, const float (&g)[TS][16],
+                                          const float (&gs)[16], float (&h)[TS][16], const int (&id)[16], int lane,
+                                          int col, int R) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+        dsf4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v = mfma4(GT[(nt * 16 + k) * 64 + lane], gs[k], v);
+#pragma unroll
+        for (int t = 0; t < TS; ++t) {
+            dsf4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) acc = mfma4(LT[(nt * 16 + k) * 64 + lane], g[t][k], acc);
+            const int row = 16 * t + col;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int kk = 4 * nt + i;
+                const float x = acc[i] - (row == id[kk] ? v[i] : 0.f);
+                h[t][kk] = row < R ? x * dact<ACT>(h[t][kk]) : 0.f;
+            }
+        }
+    }
+}
+
+template <int TS>
+__global__ __launch_bounds__(DS_BLOCK) void k_ds_train_bwd(DSBwdParams p) {
+    __shared__ __attribute__((aligned(16))) float W[DSB_FLOATS];
+    for (int i = threadIdx.x * 4; i < DSB_FLOATS; i += DS_BLOCK * 4)
+        *reinterpret_cast<float4*>(W + i) = *reinterpret_cast<const float4*>(p.wb + i);
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * (DS_BLOCK / 64) + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * (DS_BLOCK / 64);
+    const int R = p.R;
+    const int col = lane & 15, grp = lane >> 4;
+    const int64_t plane = p.B * (int64_t)R * 64;
+    for (int64_t env = wave; env < p.B; env += nwaves) {
+        float* sv = p.setvec + env * DSV_FLOATS;
+        {
+            float h0[TS][2], m0[2];
+            const float* x = p.obs + env * (int64_t)R * 8;
+#pragma unroll
+            for (int t = 0; t < TS; ++t) {
+                const int row = 16 * t + col;
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk) h0[t][kk] = row < R ? x[row * 8 + 4 * kk + grp] : 0.f;
+            }
+            set_max_batched<TS, 1, 2>(h0, m0, col, R);
+            if (col == 0) {
+                sv[DSV_MAX0 + grp] = m0[0];
+                sv[DSV_MAX0 + 4 + grp] = m0[1];
+            }
+        }
+        if (p.actor) {
+            float a[TS][16], h[TS][16], mx[16], gs[16];
+            int id[16];
+            load_rows<TS>(p.save_actor + plane, a, env, R, col, grp);  // h2
+            set_max_idx<TS>(a, mx, id, col, R);
+            store_vec(sv + DSV_MAX2A, mx, col, grp);
+            float dl[TS];
+#pragma unroll
+            for (int t = 0; t < TS; ++t) {
+                const int row = 16 * t + col;
+                dl[t] = row < R ? p.dlogits[env * R + row] : 0.f;
+            }
+            // Lambda3 product and the set sum of dlogits, in one row reduction
+            float red[20];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                float v = 0.f;
+#pragma unroll
+                for (int t = 0; t < TS; ++t) v += dl[t] * a[t][k];
+                red[k] = v;
+            }
+            {
+                float v = 0.f;
+#pragma unroll
+                for (int t = 0; t < TS; ++t) v += dl[t];
+                red[16] = v;
+                red[17] = red[18] = red[19] = 0.f;
+            }
+            row_reduce<false>(red);
+            {
+                float ga[16];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) ga[k] = red[k];
+                store_vec(sv + DSV_GA3, ga, col, grp);
+            }
+            const float g3 = red[16];
+            // dz2 = (dlogit Lambda3 - [r == argmax] g3 Gamma3) * elu'(h2)
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int f = 16 * (k >> 2) + 4 * grp + (k & 3);
+                const float l3 = W[DSB_A3L + f], gg = g3 * W[DSB_A3G + f];
+#pragma unroll
+                for (int t = 0; t < TS; ++t) {
+                    const int row = 16 * t + col;
+                    const float x = dl[t] * l3 - (row == id[k] ? gg : 0.f);
+                    a[t][k] = row < R ? x * dact<2>(a[t][k]) : 0.f;
+                }
+            }
+            set_sum<TS>(a, gs);
+            store_rows<TS, 1>(p.gz_actor, a, env, p.B, R, col, grp);
+            store_vec(sv + DSV_GS2A, gs, col, grp);
+            load_rows<TS>(p.save_actor, h, env, R, col, grp);  // h1
+            set_max_idx<TS>(h, mx, id, col, R);
+            store_vec(sv + DSV_MAX1A, mx, col, grp);
+            eq_back64<TS, 1>(W + DSB_A2LT, W + DSB_A2GT, a, gs, h, id, lane, col, R);
+            set_sum<TS>(h, gs);
+            store_rows<TS, 1>(p.gz_actor + plane, h, env, p.B, R, col, grp);
+            store_vec(sv + DSV_GS1A, gs, col, grp);
+        }
+        if (p.critic) {
+            float a[TS][16], h[TS][16], mx[16], gs[16], u[16], vv[16];
+            int id[16];
+            {
+                float gm[16];
+                const float* q = p.dmean + env * 64 + 4 * grp;
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt) {
+                    const float4 v = *reinterpret_cast<const float4*>(q + 16 * nt);
+                    gm[4 * nt] = v.x;
+                    gm[4 * nt + 1] = v.y;
+                    gm[4 * nt + 2] = v.z;
+                    gm[4 * nt + 3] = v.w;
+                }
+                // d psi[r] = dmean / R on every row: u = Lambda3^T dmean / R (row-independent),
+                // vv = Gamma3^T (sum_r d psi[r]) = Gamma3^T dmean
+                const float invR = 1.0f / (float)R;
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt) {
+                    dsf4 uu = {0.f, 0.f, 0.f, 0.f}, w = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) {
+                        uu = mfma4(W[DSB_C3LT + (nt * 16 + k) * 64 + lane], gm[k] * invR, uu);
+                        w = mfma4(W[DSB_C3GT + (nt * 16 + k) * 64 + lane], gm[k], w);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        u[4 * nt + i] = uu[i];
+                        vv[4 * nt + i] = w[i];
+                    }
+                }
+            }
+            load_rows<TS>(p.save_critic + plane, a, env, R, col, grp);  // c2
+            set_max_idx<TS>(a, mx, id, col, R);
+            store_vec(sv + DSV_MAX2C, mx, col, grp);
+            set_sum<TS>(a, gs);
+            store_vec(sv + DSV_CS2, gs, col, grp);
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+#pragma unroll
+                for (int t = 0; t < TS; ++t) {
+                    const int row = 16 * t + col;
+                    const float x = u[k] - (row == id[k] ? vv[k] : 0.f);
+                    a[t][k] = row < R ? x * dact<2>(a[t][k]) : 0.f;
+                }
+            set_sum<TS>(a, gs);
+            store_rows<TS, 1>(p.gz_critic, a, env, p.B, R, col, grp);
+            store_vec(sv + DSV_GS2C, gs, col, grp);
+            load_rows<TS>(p.save_critic, h, env, R, col, grp);  // c1
+            set_max_idx<TS>(h, mx, id, col, R);
+            store_vec(sv + DSV_MAX1C, mx, col, grp);
+            eq_back64<TS, 2>(W + DSB_C2LT, W + DSB_C2GT, a, gs, h, id, lane, col, R);
+            set_sum<TS>(h, gs);
+            store_rows<TS, 1>(p.gz_critic + plane, h, env, p.B, R, col, grp);
+            store_vec(sv + DSV_GS1C, gs, col, grp);
+        }
+    }
+}
+
+// lb_ds_pack_backward: one thread per image float; transposed fragment order for the
+// 64x64 matrices (lane l of fragment (nt, k) holds W^T[16nt + (l & 15)][in(k, l >> 4)])
+__global__ void k_ds_pack_bwd(lb_ds_weights w, float* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= DSB_FLOATS) return;
+    if (i >= DSB_A3L) {
+        const int j = i - DSB_A3L;
+        const float* v = j < 64 ? w.actor_lambda[2] : w.actor_gamma[2];
+        out[i] = v[j & 63];
+        return;
+    }
+    const float* srcs[6] = {w.actor_lambda[1], w.actor_gamma[1], w.critic_lambda[1],
+                            w.critic_gamma[1], w.critic_lambda[2], w.critic_gamma[2]};
+    const float* src = srcs[i >> 12];
+    const int idx = i & 4095;
+    const int f = idx >> 6, lane = idx & 63;
+    const int nt = f >> 4, k = f & 15;
+    const int row = 16 * nt + (lane & 15);                        // output of W^T = input of W
+    const int in = 16 * (k >> 2) + 4 * (lane >> 4) + (k & 3);     // input of W^T = output of W
+    out[i] = src ? src[in * 64 + row] : 0.f;
+}
+
+}  // namespace lbk

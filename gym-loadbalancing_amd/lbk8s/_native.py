@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblbk8s.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 LB_REWARD = {"naive": 0, "latency": 1, "fairness": 2, "multi": 3}
 LB_RNG_PHILOX, LB_RNG_TRACE = 0, 1
@@ -52,6 +52,10 @@ class LBDSWeightsC(C.Structure):
 
 LB_DS_FRAG_FLOATS = 33860
 LB_DS_MAX_ELEMENTS = 80
+LB_DS_BWD_FLOATS = 24704
+LB_DS_SETVEC_FLOATS = 648
+LB_DSV = {"MAX0": 0, "GA3": 8, "MAX2A": 72, "GS2A": 136, "MAX1A": 200, "GS1A": 264, "CS2": 328,
+          "MAX2C": 392, "GS2C": 456, "MAX1C": 520, "GS1C": 584}
 
 _lib = None
 
@@ -87,8 +91,12 @@ def lib():
     L.lb_status.argtypes = [vp, cfgp, i64, vp, vp]
     L.lb_ds_pack.argtypes = [C.POINTER(LBDSWeightsC), vp, vp]
     L.lb_ds_forward.argtypes = [vp, vp, i64, i32, vp, vp, vp]
+    L.lb_ds_train_forward.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp]
+    L.lb_ds_pack_backward.argtypes = [C.POINTER(LBDSWeightsC), vp, vp]
+    L.lb_ds_train_backward.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp]
     for f in ("lb_validate_config", "lb_state_bytes", "lb_init", "lb_reset", "lb_step", "lb_policy",
-              "lb_get_field", "lb_get_stats", "lb_status", "lb_ds_pack", "lb_ds_forward"):
+              "lb_get_field", "lb_get_stats", "lb_status", "lb_ds_pack", "lb_ds_forward",
+              "lb_ds_train_forward", "lb_ds_pack_backward", "lb_ds_train_backward"):
         getattr(L, f).restype = C.c_int
     v = L.lb_abi_version()
     if v != ABI_VERSION:
@@ -109,4 +117,5 @@ def check(rc):
 
 EXPORTED_SYMBOLS = ("lb_abi_version", "lb_last_error", "lb_validate_config", "lb_state_bytes",
                     "lb_init", "lb_reset", "lb_step", "lb_policy", "lb_get_field", "lb_get_stats",
-                    "lb_status", "lb_ds_pack", "lb_ds_forward")
+                    "lb_status", "lb_ds_pack", "lb_ds_forward", "lb_ds_train_forward",
+                    "lb_ds_pack_backward", "lb_ds_train_backward")

@@ -12,7 +12,10 @@ Masks follow the reference: logits of invalid actions become -1e8 before the Cat
 
 `DeepSetAgent.act(obs)` is the rollout entry point: on a HIP device with the fused
 kernel available (lb_ds_forward in liblbk8s.so) it evaluates actor and critic in one
-launch; otherwise it runs these torch modules (training always uses autograd here).
+launch; otherwise it runs these torch modules.  Training on a HIP device
+(`DeepSetAgent.get_action_and_value` / `DQNDeepSetAgent.forward` with grad enabled) runs
+the fused training kernels (lbk8s/fused_train.py); on the CPU, autograd through these
+modules.
 """
 from typing import Optional
 
@@ -142,11 +145,21 @@ class DeepSetAgent(nn.Module):
         dist = Categorical(logits=masked_logits(self.actor(x), masks))
         return dist.mode if deterministic else dist.sample()
 
+    def actor_critic(self, x):
+        """(logits, value).  Training on a HIP device (grad enabled, covered geometry) runs
+        the fused training kernels (lbk8s/fused_train.py); otherwise the torch modules."""
+        if x.is_cuda and torch.is_grad_enabled():
+            from . import fused_train
+            if fused_train.supported(self.actor.net, x):
+                return fused_train.actor_critic(self, x)
+        return self.actor(x), self.critic(x)
+
     def get_action_and_value(self, x, action=None, masks=None):
-        dist = Categorical(logits=masked_logits(self.actor(x), masks))
+        logits, value = self.actor_critic(x)
+        dist = Categorical(logits=masked_logits(logits, masks))
         if action is None:
             action = dist.sample()
-        return action, dist.log_prob(action), dist.entropy(), self.critic(x)
+        return action, dist.log_prob(action), dist.entropy(), value
 
     @torch.no_grad()
     def act(self, x, masks=None, generator=None):
@@ -168,6 +181,10 @@ class DQNDeepSetAgent(nn.Module):
         self.q_network = EquivariantDeepSet(_in_channels(envs), hidden_channels)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if x.is_cuda and torch.is_grad_enabled():
+            from . import fused_train
+            if fused_train.supported(self.q_network.net, x):
+                return fused_train.actor_only(self, self.q_network.net, x)
         return self.q_network(x)
 
     def get_action(self, x, masks=None, deterministic: bool = True):

@@ -1,0 +1,143 @@
+"""Fused deep-sets training step: lb_ds_train_forward /
+lb_ds_train_backward in liblbk8s.so.
+
+The reference trains its networks with torch autograd through the modules of
+envs/deep_sets_agent_original.py:56-106 (ppo_deepset.py:227-263).  Here the equivariant
+stacks run as two HIP kernels per minibatch (csrc/lbk8s_ds_train.h): a forward that keeps
+the hidden activations, and a backward that walks every layer in registers (argmax of the
+set-wise max recomputed from the saved activation, data gradients on f32 MFMA) and writes
+the layer-2 / layer-1 pre-activation gradients plus per-set vectors.  What is left —
+rho (a 64-wide MLP on the set mean), the loss, and the weight gradients as GEMMs over
+rows / sets — runs in torch:
+
+    dLambda1 = dz1^T obs            dGamma1 = -(sum_r dz1)^T max_set(obs)
+    dLambda2 = dz2^T h1             dGamma2 = -(sum_r dz2)^T max_set(h1)
+    actor  dLambda3 = sum_sets sum_r dlogit[r] h2[r]     dGamma3 = -(sum_r dlogit)^T max_set(h2)
+    critic dLambda3 = (dmean / R)^T sum_r c2[r]          dGamma3 = -dmean^T max_set(c2)
+
+The pooled gradient goes to the first row attaining the max, like torch.max in the
+reference's autograd.  Covered geometry: 8 input features, 64 hidden, 1 <= R <= 80, on a
+HIP device; `supported()` says whether an input qualifies.
+"""
+import ctypes as C
+
+import torch
+
+from . import _native
+from .deepsets import splitk_weight_grad
+from . import fused
+
+SV = _native.LB_DS_SETVEC_FLOATS
+DSV = _native.LB_DSV
+
+
+def supported(actor_net, x) -> bool:
+    return fused.ENABLED and fused._geometry_ok(actor_net, x)
+
+
+def _stream(dev):
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _pack_backward(actor_net, critic, dev):
+    w, keep = fused._weights_struct(actor_net, critic)
+    bfrag = torch.empty(_native.LB_DS_BWD_FLOATS, dtype=torch.float32, device=dev)
+    _native.check(_native.lib().lb_ds_pack_backward(C.byref(w), bfrag.data_ptr(), _stream(dev)))
+    del keep  # stream-ordered
+    return bfrag
+
+
+def _vec(setvec, name, n=64):
+    o = DSV[name]
+    return setvec[:, o:o + n]
+
+
+class _FusedDeepSetsTrain(torch.autograd.Function):
+    """(x, *params) -> (logits (B, R), psi_mean (B, 64) or None).
+
+    params: the actor's 6 equivariant weights (Lambda, Gamma per layer) followed, when a
+    critic is given, by the critic psi's 6.  Gradients flow to the params only (x is data).
+    """
+
+    @staticmethod
+    def forward(ctx, x, owner, actor_net, critic, *params):
+        dev = x.device
+        B, R, _ = x.shape
+        frag = fused.packed(owner, actor_net, critic)
+        logits = torch.empty((B, R), dtype=torch.float32, device=dev)
+        save_a = torch.empty((2, B, R, 64), dtype=torch.float32, device=dev)
+        mean = save_c = None
+        if critic is not None:
+            mean = torch.empty((B, 64), dtype=torch.float32, device=dev)
+            save_c = torch.empty((2, B, R, 64), dtype=torch.float32, device=dev)
+        _native.check(_native.lib().lb_ds_train_forward(
+            frag.data_ptr(), x.data_ptr(), B, R, logits.data_ptr(), fused._ptr(mean), save_a.data_ptr(),
+            fused._ptr(save_c), _stream(dev)))
+        ctx.actor_net, ctx.critic = actor_net, critic
+        ctx.save_for_backward(x, save_a, save_c)
+        if critic is None:
+            return logits
+        return logits, mean
+
+    @staticmethod
+    def backward(ctx, dlogits, dmean=None):
+        x, save_a, save_c = ctx.saved_tensors
+        actor_net, critic = ctx.actor_net, ctx.critic
+        dev = x.device
+        B, R, _ = x.shape
+        if dlogits is None:
+            dlogits = torch.zeros((B, R), dtype=torch.float32, device=dev)
+        dlogits = dlogits.float().contiguous()
+        if critic is not None:
+            dmean = torch.zeros((B, 64), dtype=torch.float32, device=dev) if dmean is None else dmean.float().contiguous()
+        bfrag = _pack_backward(actor_net, critic, dev)
+        gz_a = torch.empty((2, B, R, 64), dtype=torch.float32, device=dev)
+        gz_c = torch.empty((2, B, R, 64), dtype=torch.float32, device=dev) if critic is not None else None
+        setvec = torch.empty((B, SV), dtype=torch.float32, device=dev)
+        _native.check(_native.lib().lb_ds_train_backward(
+            bfrag.data_ptr(), x.data_ptr(), B, R, save_a.data_ptr(), fused._ptr(save_c), dlogits.data_ptr(),
+            fused._ptr(dmean), gz_a.data_ptr(), fused._ptr(gz_c), setvec.data_ptr(), _stream(dev)))
+        x2 = x.reshape(-1, 8)
+        max0 = _vec(setvec, "MAX0", 8)
+        g3 = dlogits.sum(1)
+        grads = [
+            splitk_weight_grad(gz_a[1], x2).view(64, 8),                      # actor Lambda1
+            -(_vec(setvec, "GS1A").t() @ max0),                                # actor Gamma1
+            splitk_weight_grad(gz_a[0], save_a[0]),                            # actor Lambda2
+            -(_vec(setvec, "GS2A").t() @ _vec(setvec, "MAX1A")),               # actor Gamma2
+            _vec(setvec, "GA3").sum(0, keepdim=True),                          # actor Lambda3
+            -(g3[None, :] @ _vec(setvec, "MAX2A")),                            # actor Gamma3
+        ]
+        if critic is not None:
+            grads += [
+                splitk_weight_grad(gz_c[1], x2).view(64, 8),                  # critic Lambda1
+                -(_vec(setvec, "GS1C").t() @ max0),                            # critic Gamma1
+                splitk_weight_grad(gz_c[0], save_c[0]),                        # critic Lambda2
+                -(_vec(setvec, "GS2C").t() @ _vec(setvec, "MAX1C")),           # critic Gamma2
+                (dmean / R).t() @ _vec(setvec, "CS2"),                         # critic Lambda3
+                -(dmean.t() @ _vec(setvec, "MAX2C")),                          # critic Gamma3
+            ]
+        return (None, None, None, None) + tuple(grads)
+
+
+def _eq_params(net):
+    out = []
+    for j in (0, 2, 4):
+        out += [net[j].Lambda.weight, net[j].Gamma.weight]
+    return out
+
+
+def actor_critic(agent, x):
+    """DeepSetAgent training forward: (logits (B, R), value (B,)), differentiable w.r.t.
+    every parameter; rho runs as the agent's own torch modules on the fused psi mean."""
+    actor_net, critic = agent.actor.net, agent.critic
+    x = x.float().contiguous()
+    logits, mean = _FusedDeepSetsTrain.apply(x, agent, actor_net, critic,
+                                             *_eq_params(actor_net), *_eq_params(critic.psi))
+    return logits, critic.rho(mean).squeeze(-1)
+
+
+def actor_only(owner, actor_net, x):
+    """EquivariantDeepSet training forward (the DQN Q network): logits (B, R)."""
+    x = x.float().contiguous()
+    return _FusedDeepSetsTrain.apply(x, owner, actor_net, None, *_eq_params(actor_net))

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LBK8S_ABI_VERSION 1
+#define LBK8S_ABI_VERSION 2
 
 /* reward_function names of loadbalancer_k8s_env.py:20-31 */
 enum { LB_REWARD_NAIVE = 0, LB_REWARD_LATENCY = 1, LB_REWARD_FAIRNESS = 2, LB_REWARD_MULTI = 3 };
@@ -195,6 +195,50 @@ int lb_ds_pack(const lb_ds_weights* w, float* frag_out, void* stream);
  * value_out [B] f32 (critic; NULL = skip).  1 <= R <= LB_DS_MAX_ELEMENTS. */
 int lb_ds_forward(const float* frag, const float* obs, int64_t num_envs, int32_t num_elements,
                   float* logits_out, float* value_out, void* stream);
+
+/* ---- Fused deep-sets training -----------------------------
+ * Replaces the reference's autograd through the same modules in the PPO update
+ * (envs/ppo_deepset.py:227-263 -> deep_sets_agent_original.py:56-106).  The training
+ * step is split: lb_ds_train_forward (logits, the critic's psi mean before rho, and the
+ * hidden activations), the loss and rho in the caller (torch), lb_ds_train_backward (the
+ * pre-activation gradients of layers 2 and 1 of each head plus per-set vectors), then the
+ * weight gradients as GEMMs over those (the caller; lbk8s/fused_train.py spells them out):
+ *   dLambda1 = dz1^T obs, dLambda2 = dz2^T h1 (actor; c1 for the critic),
+ *   dGamma_l = -(per-set sum of dz_l)^T (per-set max of the layer input),
+ *   actor dLambda3 = sum_sets GA3, dGamma3 = -(sum_r dlogits)^T MAX2A,
+ *   critic dLambda3 = (dmean / R)^T CS2, dGamma3 = -dmean^T MAX2C.
+ * The pooled gradient goes to the first row attaining the set-wise max (torch.max). */
+#define LB_DS_BWD_FLOATS 24704
+#define LB_DS_SETVEC_FLOATS 648
+/* per-set vector offsets (floats) inside a LB_DS_SETVEC_FLOATS row */
+#define LB_DSV_MAX0 0   /* [8] */
+#define LB_DSV_GA3 8
+#define LB_DSV_MAX2A 72
+#define LB_DSV_GS2A 136
+#define LB_DSV_MAX1A 200
+#define LB_DSV_GS1A 264
+#define LB_DSV_CS2 328
+#define LB_DSV_MAX2C 392
+#define LB_DSV_GS2C 456
+#define LB_DSV_MAX1C 520
+#define LB_DSV_GS1C 584
+
+/* obs [B,R,8] -> logits_out [B,R] (actor; NULL = skip), psi_mean_out [B,64] (critic psi
+ * averaged over the set; NULL = skip), save_actor [2,B,R,64] (h1 after ReLU, h2 after ELU),
+ * save_critic [2,B,R,64] (c1, c2 after ELU).  frag: lb_ds_pack's image. */
+int lb_ds_train_forward(const float* frag, const float* obs, int64_t num_envs, int32_t num_elements,
+                        float* logits_out, float* psi_mean_out, float* save_actor, float* save_critic,
+                        void* stream);
+
+/* Pack the backward image [LB_DS_BWD_FLOATS] (transposed layer-2/3 matrices). */
+int lb_ds_pack_backward(const lb_ds_weights* w, float* bwd_frag_out, void* stream);
+
+/* dlogits [B,R] (NULL = no actor), dmean [B,64] (NULL = no critic) -> gz_actor / gz_critic
+ * [2,B,R,64] (d z2, d z1: gradients before the activation of layers 2 and 1) and setvec
+ * [B, LB_DS_SETVEC_FLOATS]. */
+int lb_ds_train_backward(const float* bwd_frag, const float* obs, int64_t num_envs, int32_t num_elements,
+                         const float* save_actor, const float* save_critic, const float* dlogits,
+                         const float* dmean, float* gz_actor, float* gz_critic, float* setvec, void* stream);
 
 #ifdef __cplusplus
 }
