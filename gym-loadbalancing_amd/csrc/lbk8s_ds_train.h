@@ -12,11 +12,14 @@
 //     registers — the set-wise max's argmax is recomputed from the saved activation, the
 //     activation derivative is taken from the activation itself (ReLU: y > 0; ELU: y > 0 ?
 //     1 : y + 1), the data gradient of each 64x64 layer is an f32 MFMA against the
-//     transposed Lambda — and writes what the weight gradients need: the layer-2 and
-//     layer-1 pre-activation gradients (row-major, for split-K GEMMs against h1 / obs) and
-//     per-set vectors (set-wise max, gradient sums over the set, the actor's last-layer
-//     and the critic's last-layer products), from which every Gamma gradient and the
-//     rank-1 last-layer gradients are small GEMMs over the sets.
+//     transposed Lambda.  The two big weight gradients of each head, dLambda2 = dz2^T h1
+//     (64x64) and dLambda1 = dz1^T obs (64x8), are accumulated over all the sets a wave
+//     visits by MFMA (contraction over rows: each 16-row tile is transposed through a
+//     per-wave LDS buffer) in accumulator registers, written once per wave into a slot of
+//     a workspace, and summed over slots by k_ds_wgrad_reduce: no per-row gradient ever
+//     reaches HBM.  Per-set vectors (set-wise max, gradient sums over the set, the
+//     last-layer products) give every Gamma gradient and the rank-1 last-layer gradients
+//     as small GEMMs over the sets.
 // Layout conventions (fragment order, accumulator layout) are those of lbk8s_deepsets.h:
 // lane l holds set element (l & 15) of each 16-row tile, and at k-step k the features
 // 16(k >> 2) + 4(l >> 4) + (k & 3).
@@ -48,6 +51,12 @@ enum : int {
     DSV_FLOATS = 648,
 };
 
+constexpr int DSB_BLOCK = 256;                       // 4 waves, 1 per SIMD: 512 registers per lane
+constexpr int DSW_FLOATS = 4608;                     // per head: dLambda2 [64][64], dLambda1 [64][8]
+constexpr int DSW_SLOTS = 1024;                      // one per wave of the fixed grid
+constexpr int DSW_GRID = DSW_SLOTS / (DSB_BLOCK / 64);
+constexpr int DST_STRIDE = 80;                       // LDS transpose row stride (floats): 16 banks per row group
+
 struct DSBwdParams {
     const float* obs;          // [B][R][8]
     const float* wb;           // backward weight image [DSB_FLOATS]
@@ -55,8 +64,7 @@ struct DSBwdParams {
     const float* save_critic;  // [2][B][R][64] c1, c2
     const float* dlogits;      // [B][R]
     const float* dmean;        // [B][64]
-    float* gz_actor;           // [2][B][R][64] dz2, dz1 (pre-activation gradients)
-    float* gz_critic;          // [2][B][R][64]
+    float* wpart;              // [DSW_SLOTS][2][DSW_FLOATS] per-wave weight-gradient partials
     float* setvec;             // [B][DSV_FLOATS]
     int64_t B;
     int R;
@@ -174,18 +182,82 @@ __device__ __forceinline__ void eq_back64(const float* LT, const float* GT, cons
     }
 }
 
-template <int TS>
-__global__ __launch_bounds__(DS_BLOCK) void k_ds_train_bwd(DSBwdParams p) {
+// stage one 16-row tile (this lane: row col, features 16nt + 4grp + i) row-major in LDS
+__device__ __forceinline__ void stage_tile(float* buf, const float (&v)[16], int col, int grp) {
+    float* q = buf + col * DST_STRIDE + 4 * grp;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+        *reinterpret_cast<float4*>(q + 16 * nt) = make_float4(v[4 * nt], v[4 * nt + 1], v[4 * nt + 2], v[4 * nt + 3]);
+}
+
+// acc[mt][nt] += dz^T h over one staged 16-row tile: MFMA k-step c contracts rows
+// 4c..4c+3; A[m][kk] = dz[4c + kk][16mt + m], B[kk][n] = h[4c + kk][16nt + n]
+__device__ __forceinline__ void wgrad64(const float* la, const float* lb, dsf4 (&acc)[4][4], int col, int grp) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        float av[4], bv[4];
+        const int r = (4 * c + grp) * DST_STRIDE + col;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            av[m] = la[r + 16 * m];
+            bv[m] = lb[r + 16 * m];
+        }
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma4(av[mt], bv[nt], acc[mt][nt]);
+    }
+}
+
+// acc[mt] += dz^T obs over one staged tile (B columns 8..15 are zero)
+__device__ __forceinline__ void wgrad8(const float* la, const float* x, int64_t env, int R, int t, dsf4 (&acc)[4],
+                                       int col, int grp) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int row = 16 * t + 4 * c + grp;
+        const float xv = (col < 8 && row < R) ? x[(env * (int64_t)R + row) * 8 + col] : 0.f;
+        const int r = (4 * c + grp) * DST_STRIDE + col;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[mt] = mfma4(la[r + 16 * mt], xv, acc[mt]);
+    }
+}
+
+__device__ __forceinline__ void wpart_store(float* wp, const dsf4 (&a2)[4][4], const dsf4 (&a1)[4], int col, int grp) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int o = 16 * mt + 4 * grp + i;
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) wp[o * 64 + 16 * nt + col] = a2[mt][nt][i];
+            if (col < 8) wp[4096 + o * 8 + col] = a1[mt][i];
+        }
+}
+
+// one launch per head (HEAD 0 actor, 1 critic): a head's 80 accumulator registers, its
+// two activation tiles and the set-wise bookkeeping fit the 512 registers of a wave
+template <int TS, int HEAD>
+__global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
     __shared__ __attribute__((aligned(16))) float W[DSB_FLOATS];
-    for (int i = threadIdx.x * 4; i < DSB_FLOATS; i += DS_BLOCK * 4)
+    __shared__ __attribute__((aligned(16))) float TB[DSB_BLOCK / 64][2][16 * DST_STRIDE];
+    for (int i = threadIdx.x * 4; i < DSB_FLOATS; i += DSB_BLOCK * 4)
         *reinterpret_cast<float4*>(W + i) = *reinterpret_cast<const float4*>(p.wb + i);
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const int64_t wave = (int64_t)blockIdx.x * (DS_BLOCK / 64) + (threadIdx.x >> 6);
-    const int64_t nwaves = (int64_t)gridDim.x * (DS_BLOCK / 64);
+    const int64_t wave = (int64_t)blockIdx.x * (DSB_BLOCK / 64) + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * (DSB_BLOCK / 64);
+    float* la = TB[threadIdx.x >> 6][0];
+    float* lb = TB[threadIdx.x >> 6][1];
     const int R = p.R;
     const int col = lane & 15, grp = lane >> 4;
     const int64_t plane = p.B * (int64_t)R * 64;
+    dsf4 w2[4][4], w1[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) w2[mt][nt] = dsf4{0.f, 0.f, 0.f, 0.f};
+        w1[mt] = dsf4{0.f, 0.f, 0.f, 0.f};
+    }
     for (int64_t env = wave; env < p.B; env += nwaves) {
         float* sv = p.setvec + env * DSV_FLOATS;
         {
@@ -203,7 +275,7 @@ __global__ __launch_bounds__(DS_BLOCK) void k_ds_train_bwd(DSBwdParams p) {
                 sv[DSV_MAX0 + 4 + grp] = m0[1];
             }
         }
-        if (p.actor) {
+        if (HEAD == 0) {
             float a[TS][16], h[TS][16], mx[16], gs[16];
             int id[16];
             load_rows<TS>(p.save_actor + plane, a, env, R, col, grp);  // h2
@@ -252,17 +324,26 @@ __global__ __launch_bounds__(DS_BLOCK) void k_ds_train_bwd(DSBwdParams p) {
                 }
             }
             set_sum<TS>(a, gs);
-            store_rows<TS, 1>(p.gz_actor, a, env, p.B, R, col, grp);
             store_vec(sv + DSV_GS2A, gs, col, grp);
             load_rows<TS>(p.save_actor, h, env, R, col, grp);  // h1
             set_max_idx<TS>(h, mx, id, col, R);
             store_vec(sv + DSV_MAX1A, mx, col, grp);
+#pragma unroll
+            for (int t = 0; t < TS; ++t) {
+                stage_tile(la, a[t], col, grp);
+                stage_tile(lb, h[t], col, grp);
+                wgrad64(la, lb, w2, col, grp);
+            }
             eq_back64<TS, 1>(W + DSB_A2LT, W + DSB_A2GT, a, gs, h, id, lane, col, R);
             set_sum<TS>(h, gs);
-            store_rows<TS, 1>(p.gz_actor + plane, h, env, p.B, R, col, grp);
             store_vec(sv + DSV_GS1A, gs, col, grp);
+#pragma unroll
+            for (int t = 0; t < TS; ++t) {
+                stage_tile(la, h[t], col, grp);
+                wgrad8(la, p.obs, env, R, t, w1, col, grp);
+            }
         }
-        if (p.critic) {
+        if (HEAD == 1) {
             float a[TS][16], h[TS][16], mx[16], gs[16], u[16], vv[16];
             int id[16];
             {
@@ -308,16 +389,54 @@ __global__ __launch_bounds__(DS_BLOCK) void k_ds_train_bwd(DSBwdParams p) {
                     a[t][k] = row < R ? x * dact<2>(a[t][k]) : 0.f;
                 }
             set_sum<TS>(a, gs);
-            store_rows<TS, 1>(p.gz_critic, a, env, p.B, R, col, grp);
             store_vec(sv + DSV_GS2C, gs, col, grp);
             load_rows<TS>(p.save_critic, h, env, R, col, grp);  // c1
             set_max_idx<TS>(h, mx, id, col, R);
             store_vec(sv + DSV_MAX1C, mx, col, grp);
+#pragma unroll
+            for (int t = 0; t < TS; ++t) {
+                stage_tile(la, a[t], col, grp);
+                stage_tile(lb, h[t], col, grp);
+                wgrad64(la, lb, w2, col, grp);
+            }
             eq_back64<TS, 2>(W + DSB_C2LT, W + DSB_C2GT, a, gs, h, id, lane, col, R);
             set_sum<TS>(h, gs);
-            store_rows<TS, 1>(p.gz_critic + plane, h, env, p.B, R, col, grp);
             store_vec(sv + DSV_GS1C, gs, col, grp);
+#pragma unroll
+            for (int t = 0; t < TS; ++t) {
+                stage_tile(la, h[t], col, grp);
+                wgrad8(la, p.obs, env, R, t, w1, col, grp);
+            }
         }
+    }
+    // every wave of the fixed grid owns one slot (zeros if it saw no set)
+    wpart_store(p.wpart + wave * (2 * DSW_FLOATS) + HEAD * DSW_FLOATS, w2, w1, col, grp);
+}
+
+// sum of the per-wave partials: out[j] = sum_s wpart[s][j], j < 2 * DSW_FLOATS; zeros for
+// a head that was not run.  Block = 64 outputs x 8 slot groups (each thread sums every 8th
+// slot), combined through LDS in a fixed order: deterministic, and 1,152 blocks x 128
+// loads per thread instead of one 1,024-long chain per output.
+constexpr int DSR_COLS = 64, DSR_GROUPS = 8;
+__global__ __launch_bounds__(DSR_COLS * DSR_GROUPS) void k_ds_wgrad_reduce(const float* wpart, float* out, int actor,
+                                                                           int critic) {
+    __shared__ float part[DSR_GROUPS][DSR_COLS];
+    const int c = threadIdx.x % DSR_COLS, g = threadIdx.x / DSR_COLS;
+    const int j = blockIdx.x * DSR_COLS + c;
+    const bool live = j < 2 * DSW_FLOATS && (j < DSW_FLOATS ? actor : critic);
+    float s0 = 0.f, s1 = 0.f;
+    if (live)
+        for (int s = g; s < DSW_SLOTS; s += 2 * DSR_GROUPS) {
+            s0 += wpart[(int64_t)s * (2 * DSW_FLOATS) + j];
+            s1 += wpart[(int64_t)(s + DSR_GROUPS) * (2 * DSW_FLOATS) + j];
+        }
+    part[g][c] = s0 + s1;
+    __syncthreads();
+    if (g == 0 && j < 2 * DSW_FLOATS) {
+        float t = 0.f;
+#pragma unroll
+        for (int k = 0; k < DSR_GROUPS; ++k) t += part[k][c];
+        out[j] = live ? t : 0.f;
     }
 }
 

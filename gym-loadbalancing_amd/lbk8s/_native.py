@@ -54,6 +54,8 @@ LB_DS_FRAG_FLOATS = 33860
 LB_DS_MAX_ELEMENTS = 80
 LB_DS_BWD_FLOATS = 24704
 LB_DS_SETVEC_FLOATS = 648
+LB_DS_WGRAD_FLOATS = 4608
+LB_DS_WORKSPACE_FLOATS = 1024 * 2 * LB_DS_WGRAD_FLOATS
 LB_DSV = {"MAX0": 0, "GA3": 8, "MAX2A": 72, "GS2A": 136, "MAX1A": 200, "GS1A": 264, "CS2": 328,
           "MAX2C": 392, "GS2C": 456, "MAX1C": 520, "GS1C": 584}
 

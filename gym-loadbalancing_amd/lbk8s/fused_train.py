@@ -5,13 +5,14 @@ The reference trains its networks with torch autograd through the modules of
 envs/deep_sets_agent_original.py:56-106 (ppo_deepset.py:227-263).  Here the equivariant
 stacks run as two HIP kernels per minibatch (csrc/lbk8s_ds_train.h): a forward that keeps
 the hidden activations, and a backward that walks every layer in registers (argmax of the
-set-wise max recomputed from the saved activation, data gradients on f32 MFMA) and writes
-the layer-2 / layer-1 pre-activation gradients plus per-set vectors.  What is left —
-rho (a 64-wide MLP on the set mean), the loss, and the weight gradients as GEMMs over
-rows / sets — runs in torch:
+set-wise max recomputed from the saved activation, data gradients on f32 MFMA) and
+accumulates each head's dLambda2 / dLambda1 over all rows in MFMA accumulators (no
+per-row gradient reaches HBM), plus per-set vectors.  What is left — rho (a 64-wide MLP
+on the set mean), the loss, and the remaining weight gradients as small GEMMs over the
+sets — runs in torch:
 
-    dLambda1 = dz1^T obs            dGamma1 = -(sum_r dz1)^T max_set(obs)
-    dLambda2 = dz2^T h1             dGamma2 = -(sum_r dz2)^T max_set(h1)
+    dLambda1 = dz1^T obs (kernel)   dGamma1 = -(sum_r dz1)^T max_set(obs)
+    dLambda2 = dz2^T h1  (kernel)   dGamma2 = -(sum_r dz2)^T max_set(h1)
     actor  dLambda3 = sum_sets sum_r dlogit[r] h2[r]     dGamma3 = -(sum_r dlogit)^T max_set(h2)
     critic dLambda3 = (dmean / R)^T sum_r c2[r]          dGamma3 = -dmean^T max_set(c2)
 
@@ -24,7 +25,6 @@ import ctypes as C
 import torch
 
 from . import _native
-from .deepsets import splitk_weight_grad
 from . import fused
 
 SV = _native.LB_DS_SETVEC_FLOATS
@@ -47,9 +47,38 @@ def _pack_backward(actor_net, critic, dev):
     return bfrag
 
 
+_work = {}
+
+
+def _workspace(dev):
+    """Per-device scratch for the backward's per-wave partial sums (stream-ordered reuse)."""
+    w = _work.get(dev)
+    if w is None:
+        w = _work[dev] = torch.empty(_native.LB_DS_WORKSPACE_FLOATS, dtype=torch.float32, device=dev)
+    return w
+
+
 def _vec(setvec, name, n=64):
     o = DSV[name]
     return setvec[:, o:o + n]
+
+
+SET_CHUNK = 512  # sets per partial product of a reduction over the sets
+
+
+def _over_sets(a, b):
+    """a^T b for a (S, M), b (S, N): a reduction over S sets, split into chunk GEMMs plus a
+    sum so hipBLASLt gets ~S/512 independent tiles instead of one or two (a 51,200-long K
+    with a 64 x 64 output ran on two workgroups: 230 us; chunked: a few us)."""
+    S = a.shape[0]
+    n = S // SET_CHUNK
+    if n < 2:
+        return a.t() @ b
+    m = n * SET_CHUNK
+    out = torch.bmm(a[:m].reshape(n, SET_CHUNK, -1).transpose(1, 2), b[:m].reshape(n, SET_CHUNK, -1)).sum(0)
+    if m < S:
+        out += a[m:].t() @ b[m:]
+    return out
 
 
 class _FusedDeepSetsTrain(torch.autograd.Function):
@@ -91,31 +120,30 @@ class _FusedDeepSetsTrain(torch.autograd.Function):
         if critic is not None:
             dmean = torch.zeros((B, 64), dtype=torch.float32, device=dev) if dmean is None else dmean.float().contiguous()
         bfrag = _pack_backward(actor_net, critic, dev)
-        gz_a = torch.empty((2, B, R, 64), dtype=torch.float32, device=dev)
-        gz_c = torch.empty((2, B, R, 64), dtype=torch.float32, device=dev) if critic is not None else None
+        wgrad = torch.empty((2, _native.LB_DS_WGRAD_FLOATS), dtype=torch.float32, device=dev)
+        work = _workspace(dev)
         setvec = torch.empty((B, SV), dtype=torch.float32, device=dev)
         _native.check(_native.lib().lb_ds_train_backward(
             bfrag.data_ptr(), x.data_ptr(), B, R, save_a.data_ptr(), fused._ptr(save_c), dlogits.data_ptr(),
-            fused._ptr(dmean), gz_a.data_ptr(), fused._ptr(gz_c), setvec.data_ptr(), _stream(dev)))
-        x2 = x.reshape(-1, 8)
+            fused._ptr(dmean), wgrad.data_ptr(), work.data_ptr(), setvec.data_ptr(), _stream(dev)))
         max0 = _vec(setvec, "MAX0", 8)
         g3 = dlogits.sum(1)
         grads = [
-            splitk_weight_grad(gz_a[1], x2).view(64, 8),                      # actor Lambda1
-            -(_vec(setvec, "GS1A").t() @ max0),                                # actor Gamma1
-            splitk_weight_grad(gz_a[0], save_a[0]),                            # actor Lambda2
-            -(_vec(setvec, "GS2A").t() @ _vec(setvec, "MAX1A")),               # actor Gamma2
+            wgrad[0, 4096:].view(64, 8),                                       # actor Lambda1
+            -_over_sets(_vec(setvec, "GS1A"), max0),                           # actor Gamma1
+            wgrad[0, :4096].view(64, 64),                                      # actor Lambda2
+            -_over_sets(_vec(setvec, "GS2A"), _vec(setvec, "MAX1A")),          # actor Gamma2
             _vec(setvec, "GA3").sum(0, keepdim=True),                          # actor Lambda3
-            -(g3[None, :] @ _vec(setvec, "MAX2A")),                            # actor Gamma3
+            -_over_sets(g3[:, None], _vec(setvec, "MAX2A")),                   # actor Gamma3
         ]
         if critic is not None:
             grads += [
-                splitk_weight_grad(gz_c[1], x2).view(64, 8),                  # critic Lambda1
-                -(_vec(setvec, "GS1C").t() @ max0),                            # critic Gamma1
-                splitk_weight_grad(gz_c[0], save_c[0]),                        # critic Lambda2
-                -(_vec(setvec, "GS2C").t() @ _vec(setvec, "MAX1C")),           # critic Gamma2
-                (dmean / R).t() @ _vec(setvec, "CS2"),                         # critic Lambda3
-                -(dmean.t() @ _vec(setvec, "MAX2C")),                          # critic Gamma3
+                wgrad[1, 4096:].view(64, 8),                                   # critic Lambda1
+                -_over_sets(_vec(setvec, "GS1C"), max0),                       # critic Gamma1
+                wgrad[1, :4096].view(64, 64),                                  # critic Lambda2
+                -_over_sets(_vec(setvec, "GS2C"), _vec(setvec, "MAX1C")),      # critic Gamma2
+                _over_sets(dmean / R, _vec(setvec, "CS2")),                    # critic Lambda3
+                -_over_sets(dmean, _vec(setvec, "MAX2C")),                     # critic Gamma3
             ]
         return (None, None, None, None) + tuple(grads)
 

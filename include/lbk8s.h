@@ -200,16 +200,18 @@ int lb_ds_forward(const float* frag, const float* obs, int64_t num_envs, int32_t
  * Replaces the reference's autograd through the same modules in the PPO update
  * (envs/ppo_deepset.py:227-263 -> deep_sets_agent_original.py:56-106).  The training
  * step is split: lb_ds_train_forward (logits, the critic's psi mean before rho, and the
- * hidden activations), the loss and rho in the caller (torch), lb_ds_train_backward (the
- * pre-activation gradients of layers 2 and 1 of each head plus per-set vectors), then the
- * weight gradients as GEMMs over those (the caller; lbk8s/fused_train.py spells them out):
- *   dLambda1 = dz1^T obs, dLambda2 = dz2^T h1 (actor; c1 for the critic),
+ * hidden activations), the loss and rho in the caller (torch), lb_ds_train_backward (each
+ * head's dLambda2 = dz2^T h1 and dLambda1 = dz1^T obs, accumulated in the kernel, plus
+ * per-set vectors), then the remaining weight gradients as small GEMMs over the sets
+ * (the caller; lbk8s/fused_train.py spells them out):
  *   dGamma_l = -(per-set sum of dz_l)^T (per-set max of the layer input),
  *   actor dLambda3 = sum_sets GA3, dGamma3 = -(sum_r dlogits)^T MAX2A,
  *   critic dLambda3 = (dmean / R)^T CS2, dGamma3 = -dmean^T MAX2C.
  * The pooled gradient goes to the first row attaining the set-wise max (torch.max). */
 #define LB_DS_BWD_FLOATS 24704
 #define LB_DS_SETVEC_FLOATS 648
+#define LB_DS_WGRAD_FLOATS 4608  /* per head: dLambda2 [64][64] then dLambda1 [64][8] */
+#define LB_DS_WORKSPACE_FLOATS (1024 * 2 * LB_DS_WGRAD_FLOATS)
 /* per-set vector offsets (floats) inside a LB_DS_SETVEC_FLOATS row */
 #define LB_DSV_MAX0 0   /* [8] */
 #define LB_DSV_GA3 8
@@ -233,12 +235,15 @@ int lb_ds_train_forward(const float* frag, const float* obs, int64_t num_envs, i
 /* Pack the backward image [LB_DS_BWD_FLOATS] (transposed layer-2/3 matrices). */
 int lb_ds_pack_backward(const lb_ds_weights* w, float* bwd_frag_out, void* stream);
 
-/* dlogits [B,R] (NULL = no actor), dmean [B,64] (NULL = no critic) -> gz_actor / gz_critic
- * [2,B,R,64] (d z2, d z1: gradients before the activation of layers 2 and 1) and setvec
- * [B, LB_DS_SETVEC_FLOATS]. */
+/* dlogits [B,R] (NULL = no actor), dmean [B,64] (NULL = no critic) -> wgrad_out
+ * [2, LB_DS_WGRAD_FLOATS] (actor, critic: dLambda2, dLambda1; a head not asked for gets
+ * zeros) and setvec [B, LB_DS_SETVEC_FLOATS]; workspace [LB_DS_WORKSPACE_FLOATS] is
+ * scratch (per-wave partial sums, reduced in a fixed order: results do not depend on B's
+ * split over waves beyond float summation order). */
 int lb_ds_train_backward(const float* bwd_frag, const float* obs, int64_t num_envs, int32_t num_elements,
                          const float* save_actor, const float* save_critic, const float* dlogits,
-                         const float* dmean, float* gz_actor, float* gz_critic, float* setvec, void* stream);
+                         const float* dmean, float* wgrad_out, float* workspace, float* setvec,
+                         void* stream);
 
 #ifdef __cplusplus
 }
