@@ -102,10 +102,13 @@ __device__ __forceinline__ void store_vec(float* dst, const float (&v)[16], int 
         *reinterpret_cast<float4*>(dst + 16 * nt + 4 * grp) = make_float4(v[4 * nt], v[4 * nt + 1], v[4 * nt + 2], v[4 * nt + 3]);
 }
 
+// argmax rows (< 80) of 16 features, one byte each: id[k >> 2] byte (k & 3)
+__device__ __forceinline__ int id_of(const int (&id)[4], int k) { return (id[k >> 2] >> (8 * (k & 3))) & 0xff; }
+
 // per feature: max over the set's valid rows and the FIRST row attaining it (torch.max's
 // index, where the reference's autograd sends the pooled gradient)
 template <int TS>
-__device__ __forceinline__ void set_max_idx(const float (&h)[TS][16], float (&mx)[16], int (&id)[16], int col, int R) {
+__device__ __forceinline__ void set_max_idx(const float (&h)[TS][16], float (&mx)[16], int (&id)[4], int col, int R) {
     float m[16], c[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -128,10 +131,10 @@ __device__ __forceinline__ void set_max_idx(const float (&h)[TS][16], float (&mx
     }
     row_reduce<true>(c);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        mx[k] = m[k];
-        id[k] = (int)(-c[k]);
-    }
+    for (int k = 0; k < 16; ++k) mx[k] = m[k];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        id[q] = (int)(-c[4 * q]) | ((int)(-c[4 * q + 1]) << 8) | ((int)(-c[4 * q + 2]) << 16) | ((int)(-c[4 * q + 3]) << 24);
 }
 
 // sum over the set (rows past R hold 0)
@@ -159,7 +162,7 @@ __device__ __forceinline__ float dact(float y) {
 //   dz_prev  = dh * act'(h)
 template <int TS, int ACT>
 __device__ __forceinline__ void eq_back64(const float* LT, const float* GT, const float (&g)[TS][16],
-                                          const float (&gs)[16], float (&h)[TS][16], const int (&id)[16], int lane,
+                                          const float (&gs)[16], float (&h)[TS][16], const int (&id)[4], int lane,
                                           int col, int R) {
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
@@ -175,7 +178,7 @@ __device__ __forceinline__ void eq_back64(const float* LT, const float* GT, cons
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int kk = 4 * nt + i;
-                const float x = acc[i] - (row == id[kk] ? v[i] : 0.f);
+                const float x = acc[i] - (row == id_of(id, kk) ? v[i] : 0.f);
                 h[t][kk] = row < R ? x * dact<ACT>(h[t][kk]) : 0.f;
             }
         }
@@ -209,16 +212,54 @@ __device__ __forceinline__ void wgrad64(const float* la, const float* lb, dsf4 (
     }
 }
 
-// acc[mt] += dz^T obs over one staged tile (B columns 8..15 are zero)
-__device__ __forceinline__ void wgrad8(const float* la, const float* x, int64_t env, int R, int t, dsf4 (&acc)[4],
+// acc[mt] += dz^T obs over one staged tile: the tile's observation rows (h0: this lane holds
+// features 4kk + grp of row col) are staged next to it, B columns 8..15 read as zero
+template <int TS>
+__device__ __forceinline__ void wgrad8(const float* la, float* lb, const float (&h0)[TS][2], int t, dsf4 (&acc)[4],
                                        int col, int grp) {
+    lb[col * DST_STRIDE + grp] = h0[t][0];
+    lb[col * DST_STRIDE + 4 + grp] = h0[t][1];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        const int row = 16 * t + 4 * c + grp;
-        const float xv = (col < 8 && row < R) ? x[(env * (int64_t)R + row) * 8 + col] : 0.f;
         const int r = (4 * c + grp) * DST_STRIDE + col;
+        const float xv = col < 8 ? lb[r] : 0.f;
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) acc[mt] = mfma4(la[r + 16 * mt], xv, acc[mt]);
+    }
+}
+
+// a set's observation in fragment layout: h0[t][kk] = feature 4kk + grp of row 16t + col
+template <int TS>
+__device__ __forceinline__ void load_obs(const float* obs, int64_t env, int R, int col, int grp, float (&h0)[TS][2]) {
+    const float* x = obs + env * (int64_t)R * 8;
+#pragma unroll
+    for (int t = 0; t < TS; ++t) {
+        const int row = 16 * t + col;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) h0[t][kk] = row < R ? x[row * 8 + 4 * kk + grp] : 0.f;
+    }
+}
+
+// the head's upstream gradient for one set: actor dlogits rows (dl), critic dmean (gm, k layout)
+template <int TS, int HEAD>
+__device__ __forceinline__ void load_upstream(const DSBwdParams& p, int64_t env, int col, int grp, float (&dl)[TS],
+                                              float (&gm)[16]) {
+    if (HEAD == 0) {
+#pragma unroll
+        for (int t = 0; t < TS; ++t) {
+            const int row = 16 * t + col;
+            dl[t] = row < p.R ? p.dlogits[env * p.R + row] : 0.f;
+        }
+    } else {
+        const float* q = p.dmean + env * 64 + 4 * grp;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            const float4 v = *reinterpret_cast<const float4*>(q + 16 * nt);
+            gm[4 * nt] = v.x;
+            gm[4 * nt + 1] = v.y;
+            gm[4 * nt + 2] = v.z;
+            gm[4 * nt + 3] = v.w;
+        }
     }
 }
 
@@ -234,8 +275,11 @@ __device__ __forceinline__ void wpart_store(float* wp, const dsf4 (&a2)[4][4], c
         }
 }
 
-// one launch per head (HEAD 0 actor, 1 critic): a head's 80 accumulator registers, its
-// two activation tiles and the set-wise bookkeeping fit the 512 registers of a wave
+// One launch per head (HEAD 0 actor, 1 critic): a head's 80 accumulator registers, its two
+// activation tiles and the set-wise bookkeeping fit the 512 registers of a wave.  With one
+// wave per SIMD nothing else hides memory latency, so the loop is software-pipelined: the
+// next set's layer-2 input is loaded as soon as the layer-2 tile is dead (after the data
+// gradient), its layer-1 input and observation once the dLambda1 tiles are done.
 template <int TS, int HEAD>
 __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
     __shared__ __attribute__((aligned(16))) float W[DSB_FLOATS];
@@ -251,6 +295,9 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
     const int R = p.R;
     const int col = lane & 15, grp = lane >> 4;
     const int64_t plane = p.B * (int64_t)R * 64;
+    const float* in1 = HEAD == 0 ? p.save_actor : p.save_critic;  // h1 / c1
+    const float* in2 = in1 + plane;                                 // h2 / c2
+    const bool do_max0 = HEAD == 0 || !p.actor;
     dsf4 w2[4][4], w1[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
@@ -258,35 +305,22 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
         for (int nt = 0; nt < 4; ++nt) w2[mt][nt] = dsf4{0.f, 0.f, 0.f, 0.f};
         w1[mt] = dsf4{0.f, 0.f, 0.f, 0.f};
     }
-    for (int64_t env = wave; env < p.B; env += nwaves) {
+    float a[TS][16], h[TS][16], h0[TS][2], dl[TS], gm[16];
+    int64_t env = wave;
+    if (env < p.B) {
+        load_rows<TS>(in2, a, env, R, col, grp);
+        load_upstream<TS, HEAD>(p, env, col, grp, dl, gm);
+        load_rows<TS>(in1, h, env, R, col, grp);
+        load_obs<TS>(p.obs, env, R, col, grp, h0);
+    }
+    for (; env < p.B; env += nwaves) {
+        const int64_t nxt = env + nwaves;
         float* sv = p.setvec + env * DSV_FLOATS;
-        {
-            float h0[TS][2], m0[2];
-            const float* x = p.obs + env * (int64_t)R * 8;
-#pragma unroll
-            for (int t = 0; t < TS; ++t) {
-                const int row = 16 * t + col;
-#pragma unroll
-                for (int kk = 0; kk < 2; ++kk) h0[t][kk] = row < R ? x[row * 8 + 4 * kk + grp] : 0.f;
-            }
-            set_max_batched<TS, 1, 2>(h0, m0, col, R);
-            if (col == 0) {
-                sv[DSV_MAX0 + grp] = m0[0];
-                sv[DSV_MAX0 + 4 + grp] = m0[1];
-            }
-        }
+        float mx[16], gs[16];
+        int id[4];
         if (HEAD == 0) {
-            float a[TS][16], h[TS][16], mx[16], gs[16];
-            int id[16];
-            load_rows<TS>(p.save_actor + plane, a, env, R, col, grp);  // h2
             set_max_idx<TS>(a, mx, id, col, R);
             store_vec(sv + DSV_MAX2A, mx, col, grp);
-            float dl[TS];
-#pragma unroll
-            for (int t = 0; t < TS; ++t) {
-                const int row = 16 * t + col;
-                dl[t] = row < R ? p.dlogits[env * R + row] : 0.f;
-            }
             // Lambda3 product and the set sum of dlogits, in one row reduction
             float red[20];
 #pragma unroll
@@ -319,63 +353,29 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
 #pragma unroll
                 for (int t = 0; t < TS; ++t) {
                     const int row = 16 * t + col;
-                    const float x = dl[t] * l3 - (row == id[k] ? gg : 0.f);
+                    const float x = dl[t] * l3 - (row == id_of(id, k) ? gg : 0.f);
                     a[t][k] = row < R ? x * dact<2>(a[t][k]) : 0.f;
                 }
             }
-            set_sum<TS>(a, gs);
-            store_vec(sv + DSV_GS2A, gs, col, grp);
-            load_rows<TS>(p.save_actor, h, env, R, col, grp);  // h1
-            set_max_idx<TS>(h, mx, id, col, R);
-            store_vec(sv + DSV_MAX1A, mx, col, grp);
+        } else {
+            // d psi[r] = dmean / R on every row: u = Lambda3^T dmean / R (row-independent),
+            // vv = Gamma3^T (sum_r d psi[r]) = Gamma3^T dmean
+            float u[16], vv[16];
+            const float invR = 1.0f / (float)R;
 #pragma unroll
-            for (int t = 0; t < TS; ++t) {
-                stage_tile(la, a[t], col, grp);
-                stage_tile(lb, h[t], col, grp);
-                wgrad64(la, lb, w2, col, grp);
-            }
-            eq_back64<TS, 1>(W + DSB_A2LT, W + DSB_A2GT, a, gs, h, id, lane, col, R);
-            set_sum<TS>(h, gs);
-            store_vec(sv + DSV_GS1A, gs, col, grp);
+            for (int nt = 0; nt < 4; ++nt) {
+                dsf4 uu = {0.f, 0.f, 0.f, 0.f}, w = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int t = 0; t < TS; ++t) {
-                stage_tile(la, h[t], col, grp);
-                wgrad8(la, p.obs, env, R, t, w1, col, grp);
-            }
-        }
-        if (HEAD == 1) {
-            float a[TS][16], h[TS][16], mx[16], gs[16], u[16], vv[16];
-            int id[16];
-            {
-                float gm[16];
-                const float* q = p.dmean + env * 64 + 4 * grp;
-#pragma unroll
-                for (int nt = 0; nt < 4; ++nt) {
-                    const float4 v = *reinterpret_cast<const float4*>(q + 16 * nt);
-                    gm[4 * nt] = v.x;
-                    gm[4 * nt + 1] = v.y;
-                    gm[4 * nt + 2] = v.z;
-                    gm[4 * nt + 3] = v.w;
+                for (int k = 0; k < 16; ++k) {
+                    uu = mfma4(W[DSB_C3LT + (nt * 16 + k) * 64 + lane], gm[k] * invR, uu);
+                    w = mfma4(W[DSB_C3GT + (nt * 16 + k) * 64 + lane], gm[k], w);
                 }
-                // d psi[r] = dmean / R on every row: u = Lambda3^T dmean / R (row-independent),
-                // vv = Gamma3^T (sum_r d psi[r]) = Gamma3^T dmean
-                const float invR = 1.0f / (float)R;
 #pragma unroll
-                for (int nt = 0; nt < 4; ++nt) {
-                    dsf4 uu = {0.f, 0.f, 0.f, 0.f}, w = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                    for (int k = 0; k < 16; ++k) {
-                        uu = mfma4(W[DSB_C3LT + (nt * 16 + k) * 64 + lane], gm[k] * invR, uu);
-                        w = mfma4(W[DSB_C3GT + (nt * 16 + k) * 64 + lane], gm[k], w);
-                    }
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        u[4 * nt + i] = uu[i];
-                        vv[4 * nt + i] = w[i];
-                    }
+                for (int i = 0; i < 4; ++i) {
+                    u[4 * nt + i] = uu[i];
+                    vv[4 * nt + i] = w[i];
                 }
             }
-            load_rows<TS>(p.save_critic + plane, a, env, R, col, grp);  // c2
             set_max_idx<TS>(a, mx, id, col, R);
             store_vec(sv + DSV_MAX2C, mx, col, grp);
             set_sum<TS>(a, gs);
@@ -385,28 +385,44 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
 #pragma unroll
                 for (int t = 0; t < TS; ++t) {
                     const int row = 16 * t + col;
-                    const float x = u[k] - (row == id[k] ? vv[k] : 0.f);
+                    const float x = u[k] - (row == id_of(id, k) ? vv[k] : 0.f);
                     a[t][k] = row < R ? x * dact<2>(a[t][k]) : 0.f;
                 }
-            set_sum<TS>(a, gs);
-            store_vec(sv + DSV_GS2C, gs, col, grp);
-            load_rows<TS>(p.save_critic, h, env, R, col, grp);  // c1
-            set_max_idx<TS>(h, mx, id, col, R);
-            store_vec(sv + DSV_MAX1C, mx, col, grp);
+        }
+        set_sum<TS>(a, gs);
+        store_vec(sv + (HEAD == 0 ? DSV_GS2A : DSV_GS2C), gs, col, grp);
+        set_max_idx<TS>(h, mx, id, col, R);
+        store_vec(sv + (HEAD == 0 ? DSV_MAX1A : DSV_MAX1C), mx, col, grp);
 #pragma unroll
-            for (int t = 0; t < TS; ++t) {
-                stage_tile(la, a[t], col, grp);
-                stage_tile(lb, h[t], col, grp);
-                wgrad64(la, lb, w2, col, grp);
-            }
-            eq_back64<TS, 2>(W + DSB_C2LT, W + DSB_C2GT, a, gs, h, id, lane, col, R);
-            set_sum<TS>(h, gs);
-            store_vec(sv + DSV_GS1C, gs, col, grp);
+        for (int t = 0; t < TS; ++t) {
+            stage_tile(la, a[t], col, grp);
+            stage_tile(lb, h[t], col, grp);
+            wgrad64(la, lb, w2, col, grp);
+        }
+        if (HEAD == 0) eq_back64<TS, 1>(W + DSB_A2LT, W + DSB_A2GT, a, gs, h, id, lane, col, R);
+        else eq_back64<TS, 2>(W + DSB_C2LT, W + DSB_C2GT, a, gs, h, id, lane, col, R);
+        if (nxt < p.B) {  // layer-2 tile and upstream gradient are dead: prefetch the next set's
+            load_rows<TS>(in2, a, nxt, R, col, grp);
+            load_upstream<TS, HEAD>(p, nxt, col, grp, dl, gm);
+        }
+        set_sum<TS>(h, gs);
+        store_vec(sv + (HEAD == 0 ? DSV_GS1A : DSV_GS1C), gs, col, grp);
 #pragma unroll
-            for (int t = 0; t < TS; ++t) {
-                stage_tile(la, h[t], col, grp);
-                wgrad8(la, p.obs, env, R, t, w1, col, grp);
+        for (int t = 0; t < TS; ++t) {
+            stage_tile(la, h[t], col, grp);
+            wgrad8<TS>(la, lb, h0, t, w1, col, grp);
+        }
+        if (do_max0) {
+            float m0[2];
+            set_max_batched<TS, 1, 2>(h0, m0, col, R);
+            if (col == 0) {
+                sv[DSV_MAX0 + grp] = m0[0];
+                sv[DSV_MAX0 + 4 + grp] = m0[1];
             }
+        }
+        if (nxt < p.B) {
+            load_rows<TS>(in1, h, nxt, R, col, grp);
+            load_obs<TS>(p.obs, nxt, R, col, grp, h0);
         }
     }
     // every wave of the fixed grid owns one slot (zeros if it saw no set)

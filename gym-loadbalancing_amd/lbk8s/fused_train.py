@@ -148,6 +148,26 @@ class _FusedDeepSetsTrain(torch.autograd.Function):
         return (None, None, None, None) + tuple(grads)
 
 
+class _Rho(torch.autograd.Function):
+    """The critic's rho = Linear(64,64) ELU Linear(64,1) on the psi means (B, 64), with the
+    two weight gradients as chunked reductions over the sets (`_over_sets`): torch's Linear
+    backward runs them as one K = B GEMM on one or two workgroups (120-180 us each at
+    B = 51,200).  Same math as deep_sets_agent_original.py:95-97."""
+
+    @staticmethod
+    def forward(ctx, mean, w1, b1, w2, b2):
+        r1 = torch.nn.functional.elu(torch.addmm(b1, mean, w1.t()))
+        ctx.save_for_backward(mean, w1, w2, r1)
+        return torch.addmm(b2, r1, w2.t())
+
+    @staticmethod
+    def backward(ctx, gv):
+        mean, w1, w2, r1 = ctx.saved_tensors
+        gv = gv.contiguous()
+        gz = (gv @ w2) * torch.where(r1 > 0, torch.ones_like(r1), r1 + 1)
+        return gz @ w1, _over_sets(gz, mean), gz.sum(0), _over_sets(gv, r1), gv.sum(0)
+
+
 def _eq_params(net):
     out = []
     for j in (0, 2, 4):
@@ -162,7 +182,8 @@ def actor_critic(agent, x):
     x = x.float().contiguous()
     logits, mean = _FusedDeepSetsTrain.apply(x, agent, actor_net, critic,
                                              *_eq_params(actor_net), *_eq_params(critic.psi))
-    return logits, critic.rho(mean).squeeze(-1)
+    rho = critic.rho
+    return logits, _Rho.apply(mean, rho[0].weight, rho[0].bias, rho[2].weight, rho[2].bias).squeeze(-1)
 
 
 def actor_only(owner, actor_net, x):
