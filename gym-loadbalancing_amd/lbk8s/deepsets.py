@@ -156,7 +156,8 @@ class DeepSetAgent(nn.Module):
 
     def get_action_and_value(self, x, action=None, masks=None):
         logits, value = self.actor_critic(x)
-        dist = Categorical(logits=masked_logits(logits, masks))
+        # validate_args=False: argument validation syncs with the host (not capturable)
+        dist = Categorical(logits=masked_logits(logits, masks), validate_args=False)
         if action is None:
             action = dist.sample()
         return action, dist.log_prob(action), dist.entropy(), value

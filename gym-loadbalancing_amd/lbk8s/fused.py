@@ -11,9 +11,9 @@ torch parameters on the device.  The image is cached per module and rebuilt when
 parameter's version counter moves (every optimizer step bumps it), so callers never
 repack by hand.
 
-Training (the PPO / DQN losses) keeps the torch modules: autograd needs them.  Inputs the
-kernel does not cover (not on a HIP device, R > 80, non-reference widths) run the same
-torch modules on the same device; `require=True` turns that into an error instead.
+Training runs the fused training kernels (lbk8s/fused_train.py), which use the same image.
+Inputs the kernel does not cover (not on a HIP device, R > 80, non-reference widths) run
+the same torch modules on the same device; `require=True` turns that into an error instead.
 """
 import ctypes as C
 import weakref
@@ -58,12 +58,19 @@ def _geometry_ok(actor_net, x):
             and actor_net[0].Lambda.weight.shape == (64, 8) and actor_net[2].Lambda.weight.shape == (64, 64))
 
 
+def invalidate(module):
+    """Drop `module`'s cached image: needed after parameter updates the version counters do
+    not see (optimizer steps replayed from a HIP graph)."""
+    _cache.pop(module, None)
+
+
 def packed(module, actor_net, critic):
-    """Fragment image of (actor_net, critic) cached on `module`; rebuilt after any update."""
+    """Fragment image of (actor_net, critic) cached on `module`; rebuilt after any update.
+    While a HIP graph is being captured the pack is always issued (and so replayed)."""
     params = list(actor_net.parameters()) + (list(critic.parameters()) if critic is not None else [])
     version = tuple(p._version for p in params) + tuple(p.data_ptr() for p in params)
     hit = _cache.get(module)
-    if hit is not None and hit[0] == version:
+    if hit is not None and hit[0] == version and not torch.cuda.is_current_stream_capturing():
         return hit[1]
     dev = params[0].device
     frag = torch.empty(_native.LB_DS_FRAG_FLOATS, dtype=torch.float32, device=dev)

@@ -10,6 +10,12 @@ masks are all True anyway, :808-821) and the stored masks are used in the update
 
 Multi-GPU: one process per GPU, each with its own envs (LBVecEnv env_id_offset); the
 gradients are averaged with one all_reduce per optimizer step (RCCL over xGMI).
+
+On one GPU the minibatch step (loss, fused forward/backward, clip_grad_norm, Adam) is
+captured once as a HIP graph and replayed per minibatch: ~200 launches per minibatch
+otherwise leave the GPU waiting on the host between the fused kernels.  The capture's
+warm-up steps are undone (parameters restored, Adam state zeroed), so the graph path
+computes the same update as the eager one.
 """
 import time
 from typing import Optional
@@ -17,6 +23,7 @@ from typing import Optional
 import torch
 from torch import nn, optim
 
+from . import fused
 from .deepsets import DeepSetAgent, allreduce_gradients
 
 
@@ -72,7 +79,7 @@ class PPO_DeepSets:
                  update_epochs: int = 4, norm_adv: bool = True, clip_coef: float = 0.2,
                  clip_vloss: bool = True, ent_coef: float = 0.01, vf_coef: float = 0.5,
                  max_grad_norm: float = 0.5, target_kl: Optional[float] = None, seed: int = 1,
-                 device=None, log_fn=None, num_envs=None, tensorboard_log=None):
+                 device=None, log_fn=None, num_envs=None, tensorboard_log=None, use_graphs=None):
         # num_envs / tensorboard_log: accepted for signature compatibility with
         # ppo_deepset.py:53-75 (the env's num_envs is used; there is no tensorboard writer)
         self.env = env
@@ -90,7 +97,18 @@ class PPO_DeepSets:
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed)
         self.agent = DeepSetAgent(env).to(self.device)
-        self.optimizer = optim.Adam(self.agent.parameters(), lr=learning_rate, eps=1e-5)
+        if use_graphs is None:
+            import torch.distributed as dist
+            multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+            use_graphs = self.device.type == "cuda" and not multi
+        # a captured step needs equal minibatches and a device-side Adam step / lr
+        self.use_graphs = bool(use_graphs) and self.batch_size % self.minibatch_size == 0
+        if self.use_graphs:
+            self._lr = torch.tensor(float(learning_rate), device=self.device)
+            self.optimizer = optim.Adam(self.agent.parameters(), lr=self._lr, eps=1e-5, capturable=True)
+        else:
+            self.optimizer = optim.Adam(self.agent.parameters(), lr=learning_rate, eps=1e-5)
+        self._mb_graph = None
         T, B = num_steps, self.num_envs
         R, A = env.observation_space.shape[0], env.action_space.n
         dev = self.device
@@ -136,6 +154,43 @@ class PPO_DeepSets:
         self._ep_cnt.zero_()
         return next_obs, next_done
 
+    def _minibatch_step(self, obs, actions, logprobs, masks, adv, ret, val):
+        loss, pg, vl, ent, kl, cf = ppo_loss(
+            self.agent, obs, actions, logprobs, masks, adv, ret, val,
+            self.clip_coef, self.ent_coef, self.vf_coef, self.norm_adv, self.clip_vloss)
+        self.optimizer.zero_grad(set_to_none=not self.use_graphs)
+        loss.backward()
+        allreduce_gradients(self.agent)
+        nn.utils.clip_grad_norm_(self.agent.parameters(), self.max_grad_norm)
+        self.optimizer.step()
+        return loss, pg, vl, ent, kl, cf
+
+    def _capture(self, src, mb):
+        """Capture one minibatch step on static buffers (filled from minibatch `mb`)."""
+        self._static = [torch.empty((self.minibatch_size,) + t.shape[1:], dtype=t.dtype, device=t.device)
+                        for t in src]
+        for d, t in zip(self._static, src):
+            torch.index_select(t, 0, mb, out=d)
+        params = list(self.agent.parameters())
+        snap = [p.detach().clone() for p in params]
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for _ in range(2):  # warm-up: allocates grads, Adam state, workspaces
+                self._minibatch_step(*self._static)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._static_out = self._minibatch_step(*self._static)
+        with torch.no_grad():  # undo the warm-up steps
+            for p, q in zip(params, snap):
+                p.copy_(q)
+            for st in self.optimizer.state.values():
+                for v in st.values():
+                    if isinstance(v, torch.Tensor):
+                        v.zero_()
+        self._mb_graph = g
+
     def update(self, next_obs, next_done):
         with torch.no_grad():
             next_value = self.agent.get_value(next_obs).reshape(1, -1)
@@ -147,21 +202,26 @@ class PPO_DeepSets:
         b_actions = self.actions.reshape(-1)
         b_masks = self.masks.reshape(-1, self.masks.shape[-1])
         b_adv, b_ret, b_val = advantages.reshape(-1), returns.reshape(-1), self.values.reshape(-1)
+        src = (b_obs, b_actions, b_logprobs, b_masks, b_adv, b_ret, b_val)
         stats = {}
         for epoch in range(self.update_epochs):
             b_inds = torch.randperm(self.batch_size, device=self.device, generator=self.gen)
             for start in range(0, self.batch_size, self.minibatch_size):
                 mb = b_inds[start:start + self.minibatch_size]
-                loss, pg, vl, ent, kl, cf = ppo_loss(
-                    self.agent, b_obs[mb], b_actions[mb], b_logprobs[mb], b_masks[mb], b_adv[mb], b_ret[mb],
-                    b_val[mb], self.clip_coef, self.ent_coef, self.vf_coef, self.norm_adv, self.clip_vloss)
-                self.optimizer.zero_grad()
-                loss.backward()
-                allreduce_gradients(self.agent)
-                nn.utils.clip_grad_norm_(self.agent.parameters(), self.max_grad_norm)
-                self.optimizer.step()
+                if self.use_graphs:
+                    if self._mb_graph is None:
+                        self._capture(src, mb)
+                    for d, t in zip(self._static, src):
+                        torch.index_select(t, 0, mb, out=d)
+                    self._mb_graph.replay()
+                    out = self._static_out
+                else:
+                    out = self._minibatch_step(*(t[mb] for t in src))
+                loss, pg, vl, ent, kl, cf = out
             if self.target_kl is not None and kl > self.target_kl:
                 break
+        if self.use_graphs:
+            fused.invalidate(self.agent)  # replayed Adam steps do not move the version counters
         stats.update(loss=loss.item(), pg_loss=pg.item(), v_loss=vl.item(), entropy=ent.item(),
                      approx_kl=kl.item(), clipfrac=cf.item())
         return stats
@@ -177,7 +237,11 @@ class PPO_DeepSets:
         global_step = 0
         for update in range(1, num_updates + 1):
             if self.anneal_lr:
-                self.optimizer.param_groups[0]["lr"] = (1.0 - (update - 1.0) / num_updates) * self.learning_rate
+                lr = (1.0 - (update - 1.0) / num_updates) * self.learning_rate
+                if self.use_graphs:
+                    self._lr.fill_(lr)  # the captured Adam step reads the lr tensor
+                else:
+                    self.optimizer.param_groups[0]["lr"] = lr
             next_obs, next_done = self.rollout(next_obs, next_done)
             global_step += self.batch_size
             stats = self.update(next_obs, next_done)

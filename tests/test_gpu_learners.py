@@ -40,3 +40,20 @@ def test_dqn_learns_end_to_end():
     # target network was hard-synced at step 100 and 200
     assert algo.rb.full or algo.rb.pos == 300 % algo.rb.size
     assert algo.episode_returns
+
+
+def test_ppo_graph_update_matches_eager():
+    """The HIP-graph minibatch step (captured once, replayed) computes the eager update:
+    two updates, so the second rollout must see the first update's weights (the fused
+    forward's weight image is invalidated after replays the version counters miss)."""
+    from lbk8s import LBVecEnv
+    from lbk8s.ppo import PPO_DeepSets
+    res = []
+    for graphs in (False, True):
+        env = LBVecEnv(256, seed=5, as_tensors=True, episode_length=10)
+        algo = PPO_DeepSets(env, num_steps=8, n_minibatches=4, update_epochs=2, seed=2, use_graphs=graphs)
+        assert algo.use_graphs == graphs
+        algo.learn(total_timesteps=256 * 8 * 2)
+        res.append([p.detach().clone() for p in algo.agent.parameters()])
+    for a, b in zip(*res):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=2e-6)
