@@ -237,21 +237,28 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
             eq_layer<TS, P, 16, 2>(W + DS_A2L, W + DS_A2G, h1, m1, h2, lane);
             if (TRAIN) store_rows<TS, P>(p.save_actor + p.B * (int64_t)R * 64, h2, env0, p.B, R, col, grp);
             set_max_batched<TS, P, 16>(h2, m2, col, R);
-            const float* L = W + DS_A3L;
-            const float* G = W + DS_A3G;
-            dsf4 g = {0.f, 0.f, 0.f, 0.f};
+            // layer 3 (64 -> 1) on the VALU: a 16-row output tile would use 1/16 of an MFMA.
+            // Lane (col, grp) dots its 16 features with Lambda3 / -Gamma3 (row 0 of the
+            // fragments: column 0 of its row group), then the 4 row groups are summed.
+            const float* L = W + DS_A3L + 16 * grp;
+            const float* G = W + DS_A3G + 16 * grp;
+            float gl = 0.f;
 #pragma unroll
-            for (int k = 0; k < 16; ++k) g = mfma4(G[k * 64 + lane], m2[k], g);
+            for (int k = 0; k < 16; ++k) gl += G[k * 64] * m2[k];
+            gl += __shfl_xor(gl, 16);
+            gl += __shfl_xor(gl, 32);
 #pragma unroll
             for (int s = 0; s < P; ++s) {
-                const float init = from_col_dyn<P>(g[0], s);
+                const float init = from_col_dyn<P>(gl, s);
 #pragma unroll
                 for (int t = 0; t < TS; ++t) {
-                    dsf4 acc = {init, 0.f, 0.f, 0.f};
+                    float v = 0.f;
 #pragma unroll
-                    for (int k = 0; k < 16; ++k) acc = mfma4(L[k * 64 + lane], h2[s * TS + t][k], acc);
+                    for (int k = 0; k < 16; ++k) v += L[k * 64] * h2[s * TS + t][k];
+                    v += __shfl_xor(v, 16);
+                    v += __shfl_xor(v, 32);
                     const int row = 16 * t + col;
-                    if (grp == 0 && row < R && env0 + s < p.B) p.logits[(env0 + s) * R + row] = acc[0];
+                    if (grp == 0 && row < R && env0 + s < p.B) p.logits[(env0 + s) * R + row] = init + v;
                 }
             }
         }
@@ -264,12 +271,14 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
         eq_layer<TS, P, 16, 2>(W + DS_C2L, W + DS_C2G, h1, m1, h2, lane);
         if (TRAIN) store_rows<TS, P>(p.save_critic + p.B * (int64_t)R * 64, h2, env0, p.B, R, col, grp);
         set_max_batched<TS, P, 16>(h2, m2, col, R);
-        eq_layer<TS, P, 16, 0>(W + DS_C3L, W + DS_C3G, h2, m2, h1, lane);
-        // batched mean: column c carries env (c mod P)'s mean over its valid set elements
+        // layer 3 has no activation and only its mean over the set is used, so
+        // mean_r(Lambda3 c2[r] - Gamma3 max(c2)) = Lambda3 mean_r(c2) - Gamma3 max(c2): one
+        // matrix-vector pair on the batched (column c = env c mod P) operands instead of a
+        // 64x64 layer over every row
         float mean[16];
         {
             const float invR = 1.0f / (float)R;
-            float sm[16 * P];
+            float sm[16 * P], mc[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k)
 #pragma unroll
@@ -277,7 +286,7 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
                     float v = 0.f;
 #pragma unroll
                     for (int t = 0; t < TS; ++t)
-                        if (16 * t + col < R) v += h1[s * TS + t][k];
+                        if (16 * t + col < R) v += h2[s * TS + t][k];
                     sm[k * P + s] = v;
                 }
             row_reduce<false>(sm);
@@ -286,7 +295,17 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
                 float r = sm[k * P];
 #pragma unroll
                 for (int s = 1; s < P; ++s) r = (col % P == s) ? sm[k * P + s] : r;
-                mean[k] = r * invR;
+                mc[k] = r * invR;
+            }
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                dsf4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int k = 0; k < 16; ++k) acc = mfma4(W[DS_C3G + (nt * 16 + k) * 64 + lane], m2[k], acc);
+#pragma unroll
+                for (int k = 0; k < 16; ++k) acc = mfma4(W[DS_C3L + (nt * 16 + k) * 64 + lane], mc[k], acc);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) mean[4 * nt + i] = acc[i];
             }
         }
         if (TRAIN) {
