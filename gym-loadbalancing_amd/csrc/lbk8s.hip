@@ -28,6 +28,56 @@
 
 namespace lbk {
 
+// lb_replay_add: the DQN vector step's bookkeeping in one launch (dqn_deepset.py:158-174
+// replay add + obs <- next_obs, :147-156 episode returns).  Slot pos = *pos_in; one thread
+// writes (pos + 1) % slots to *pos_out, a different word (callers alternate the two), so
+// no thread of this launch can read the advanced position.
+struct ReplayParams {
+    int64_t B;
+    int f4;  // float4s per observation
+    int64_t slots;
+    const int64_t* pos_in;
+    int64_t* pos_out;
+    float4* obs;
+    const float4* next_obs;
+    const int32_t* actions;
+    const float* reward;
+    const uint8_t* done;
+    const double* ep_stats;  // [B][LB_ST_K], column 0 = the finished episode's return
+    float4* rb_obs;
+    float4* rb_next_obs;
+    int64_t* rb_actions;
+    float* rb_rewards;
+    float* rb_dones;
+    double* ep_sum;  // [B] per-env sums (deterministic; reduced when flushed)
+    double* ep_cnt;
+};
+
+__global__ void k_replay_add(ReplayParams p) {
+    const int64_t pos = *p.pos_in;
+    const int64_t n4 = p.B * p.f4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4 || i < p.B;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        if (i < n4) {
+            const float4 o = p.obs[i], nx = p.next_obs[i];
+            p.rb_obs[pos * n4 + i] = o;
+            p.rb_next_obs[pos * n4 + i] = nx;
+            p.obs[i] = nx;
+        }
+        if (i < p.B) {
+            const float d = p.done[i] ? 1.f : 0.f;
+            p.rb_actions[pos * p.B + i] = p.actions[i];
+            p.rb_rewards[pos * p.B + i] = p.reward[i];
+            p.rb_dones[pos * p.B + i] = d;
+            if (p.ep_sum && p.done[i]) {
+                p.ep_sum[i] += p.ep_stats[i * LB_ST_K];
+                p.ep_cnt[i] += 1.0;
+            }
+        }
+        if (i == 0) *p.pos_out = (pos + 1) % p.slots;
+    }
+}
+
 // LAT[k][j]: endpoint latency after j selections from trunc(initial) = k
 // (increase_endpoint_latency :1013-1023 then decrease_endpoint_latency :1052-1060 in the
 // same step); CPU[c][M]: node cpu after M selections (:861-887 then :937-960).
@@ -536,18 +586,18 @@ unsigned ds_grid(int64_t groups) {
     return (unsigned)std::min<int64_t>(want, device_cus());
 }
 
-template <bool TRAIN>
+template <int MODE>
 void ds_forward_launch(const DSParams& p, hipStream_t s) {
     // a wave takes P envs per iteration: P = 4 for R <= 16, 2 for R <= 32, else 1
     const int ts = (p.R + 15) / 16;
     const int P = ts == 1 ? 4 : (ts == 2 ? 2 : 1);
     const unsigned grid = ds_grid((p.B + P - 1) / P);
     switch (ts) {
-        case 1: hipLaunchKernelGGL((k_deepsets_fwd<1, 4, TRAIN>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
-        case 2: hipLaunchKernelGGL((k_deepsets_fwd<2, 2, TRAIN>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
-        case 3: hipLaunchKernelGGL((k_deepsets_fwd<3, 1, TRAIN>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
-        case 4: hipLaunchKernelGGL((k_deepsets_fwd<4, 1, TRAIN>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
-        default: hipLaunchKernelGGL((k_deepsets_fwd<5, 1, TRAIN>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        case 1: hipLaunchKernelGGL((k_deepsets_fwd<1, 4, MODE>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        case 2: hipLaunchKernelGGL((k_deepsets_fwd<2, 2, MODE>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        case 3: hipLaunchKernelGGL((k_deepsets_fwd<3, 1, MODE>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        case 4: hipLaunchKernelGGL((k_deepsets_fwd<4, 1, MODE>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        default: hipLaunchKernelGGL((k_deepsets_fwd<5, 1, MODE>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
     }
 }
 }  // namespace
@@ -562,8 +612,36 @@ int lb_ds_forward(const float* frag, const float* obs, int64_t num_envs, int32_t
         return fail("num_elements must be in [1, 80] (LB_DS_MAX_ELEMENTS)");
     if (!logits_out && !value_out) return 0;
     DSParams p{obs, frag, logits_out, value_out, num_envs, num_elements, logits_out != nullptr, value_out != nullptr,
-               nullptr, nullptr, nullptr};
-    ds_forward_launch<false>(p, (hipStream_t)stream);
+               nullptr, nullptr, nullptr, nullptr, nullptr};
+    ds_forward_launch<0>(p, (hipStream_t)stream);
+    return check_launch();
+}
+
+int lb_ds_q_argmax(const float* frag, const float* obs, int64_t num_envs, int32_t num_elements, const uint8_t* masks,
+                   float* q_out, int32_t* actions_out, void* stream) {
+    if (!frag || !obs || !actions_out || num_envs < 1) return fail("frag/obs/actions_out NULL or num_envs < 1");
+    if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS)
+        return fail("num_elements must be in [1, 80] (LB_DS_MAX_ELEMENTS)");
+    DSParams p{obs, frag, q_out, nullptr, num_envs, num_elements, 1, 0, nullptr, nullptr, nullptr, actions_out, masks};
+    ds_forward_launch<2>(p, (hipStream_t)stream);
+    return check_launch();
+}
+
+int lb_replay_add(int64_t num_envs, int32_t obs_floats, int64_t slots, const int64_t* pos_in, int64_t* pos_out,
+                  float* obs, const float* next_obs, const int32_t* actions, const float* reward, const uint8_t* done,
+                  const double* ep_stats, float* rb_obs, float* rb_next_obs, int64_t* rb_actions, float* rb_rewards,
+                  float* rb_dones, double* ep_sum, double* ep_cnt, void* stream) {
+    if (num_envs < 1 || obs_floats < 4 || obs_floats % 4 || slots < 1) return fail("bad replay geometry");
+    if (!pos_in || !pos_out || pos_in == pos_out || !obs || !next_obs || !actions || !reward || !done || !rb_obs ||
+        !rb_next_obs || !rb_actions || !rb_rewards || !rb_dones || ((ep_sum || ep_cnt) && !(ep_sum && ep_cnt && ep_stats)))
+        return fail("replay buffers NULL (or pos_in == pos_out)");
+    ReplayParams p{num_envs, obs_floats / 4, slots, pos_in, pos_out, reinterpret_cast<float4*>(obs),
+                   reinterpret_cast<const float4*>(next_obs), actions, reward, done, ep_stats,
+                   reinterpret_cast<float4*>(rb_obs), reinterpret_cast<float4*>(rb_next_obs), rb_actions, rb_rewards,
+                   rb_dones, ep_sum, ep_cnt};
+    const int64_t n = std::max<int64_t>(num_envs * p.f4, num_envs);
+    const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 65535);
+    hipLaunchKernelGGL(k_replay_add, dim3(grid), dim3(256), 0, (hipStream_t)stream, p);
     return check_launch();
 }
 
@@ -576,8 +654,8 @@ int lb_ds_train_forward(const float* frag, const float* obs, int64_t num_envs, i
     if ((logits_out && !save_actor) || (psi_mean_out && !save_critic))
         return fail("a head's activation buffer is NULL");
     DSParams p{obs, frag, logits_out, nullptr, num_envs, num_elements, logits_out != nullptr, psi_mean_out != nullptr,
-               save_actor, save_critic, psi_mean_out};
-    ds_forward_launch<true>(p, (hipStream_t)stream);
+               save_actor, save_critic, psi_mean_out, nullptr, nullptr};
+    ds_forward_launch<1>(p, (hipStream_t)stream);
     return check_launch();
 }
 

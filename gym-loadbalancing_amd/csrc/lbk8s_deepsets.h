@@ -40,6 +40,10 @@ struct DSParams {
     float* save_actor;    // [2][B][R][64]: actor h1 (after ReLU), h2 (after ELU)
     float* save_critic;   // [2][B][R][64]: critic c1, c2 (after ELU)
     float* psi_mean;      // [B][64]: critic psi output averaged over the set (rho runs in torch)
+    // greedy action (inference only): actions[b] = first argmax over rows of
+    // (masks[b][r] ? logits[b][r] : -1e8) (dqn_deepset.py:134-142); NULL = skip
+    int32_t* actions;
+    const uint8_t* masks;  // [B][R] or NULL (all valid)
 };
 
 // fragment layout of the packed weights (floats).  A matrix with KS input k-steps and NT
@@ -197,11 +201,16 @@ __device__ __forceinline__ void store_rows(float* plane, const float (&h)[P * TS
         }
 }
 
-template <int TS, int P, bool TRAIN>
+// MODE 0: logits / value; 1: training forward (TRAIN: activations, psi mean); 2: Q values
+// and the masked greedy action (ARGMAX; actor only)
+template <int TS, int P, int MODE>
 __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
+    constexpr bool TRAIN = MODE == 1, ARGMAX = MODE == 2;
     __shared__ __attribute__((aligned(16))) float W[DS_LDS_FLOATS];
-    // stage the weight fragments (once per block; blocks are persistent)
-    for (int i = threadIdx.x * 4; i < DS_FLOATS; i += DS_BLOCK * 4)
+    // stage the weight fragments (once per block; blocks are persistent); an actor-only
+    // launch (DQN) stages only the actor's
+    const int nstage = (ARGMAX || !p.critic) ? DS_C1L : DS_FLOATS;
+    for (int i = threadIdx.x * 4; i < nstage; i += DS_BLOCK * 4)
         *reinterpret_cast<float4*>(W + i) = *reinterpret_cast<const float4*>(p.wfrag + i);
     __syncthreads();
     const int lane = threadIdx.x & 63;
@@ -247,9 +256,12 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
             for (int k = 0; k < 16; ++k) gl += G[k * 64] * m2[k];
             gl += __shfl_xor(gl, 16);
             gl += __shfl_xor(gl, 32);
+            float best[P], brow[P];  // this lane's first masked maximum per env (argmax mode)
 #pragma unroll
             for (int s = 0; s < P; ++s) {
                 const float init = from_col_dyn<P>(gl, s);
+                best[s] = -INFINITY;
+                brow[s] = 1e9f;
 #pragma unroll
                 for (int t = 0; t < TS; ++t) {
                     float v = 0.f;
@@ -258,11 +270,35 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
                     v += __shfl_xor(v, 16);
                     v += __shfl_xor(v, 32);
                     const int row = 16 * t + col;
-                    if (grp == 0 && row < R && env0 + s < p.B) p.logits[(env0 + s) * R + row] = init + v;
+                    const bool live = row < R && env0 + s < p.B;
+                    if (grp == 0 && live && p.logits) p.logits[(env0 + s) * R + row] = init + v;
+                    if (ARGMAX && live) {
+                        const float q = (!p.masks || p.masks[(env0 + s) * R + row]) ? init + v : -1e8f;
+                        if (q > best[s]) {
+                            best[s] = q;
+                            brow[s] = (float)row;
+                        }
+                    }
+                }
+            }
+            if (ARGMAX) {
+                // over the 16 columns: the max, then the smallest row attaining it
+                float m[P], c[P];
+#pragma unroll
+                for (int s = 0; s < P; ++s) m[s] = best[s];
+                row_reduce<true>(m);
+#pragma unroll
+                for (int s = 0; s < P; ++s) c[s] = best[s] == m[s] ? -brow[s] : -1e9f;
+                row_reduce<true>(c);
+                if (lane < P && env0 + lane < p.B) {
+                    float r = -c[0];
+#pragma unroll
+                    for (int s = 1; s < P; ++s) r = lane == s ? -c[s] : r;
+                    p.actions[env0 + lane] = (int32_t)r;
                 }
             }
         }
-        if (!p.critic) continue;
+        if (ARGMAX || !p.critic) continue;
 
         // ---- critic: psi = Eq ELU Eq ELU Eq, mean over the set, rho = Linear ELU Linear
         eq_layer<TS, P, 2, 2>(W + DS_C1L, W + DS_C1G, h0, m0, h1, lane);

@@ -93,12 +93,15 @@ def lib():
     L.lb_status.argtypes = [vp, cfgp, i64, vp, vp]
     L.lb_ds_pack.argtypes = [C.POINTER(LBDSWeightsC), vp, vp]
     L.lb_ds_forward.argtypes = [vp, vp, i64, i32, vp, vp, vp]
+    L.lb_ds_q_argmax.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp]
+    L.lb_replay_add.argtypes = [i64, i32, i64] + [vp] * 15 + [vp]
     L.lb_ds_train_forward.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp]
     L.lb_ds_pack_backward.argtypes = [C.POINTER(LBDSWeightsC), vp, vp]
     L.lb_ds_train_backward.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp]
     for f in ("lb_validate_config", "lb_state_bytes", "lb_init", "lb_reset", "lb_step", "lb_policy",
               "lb_get_field", "lb_get_stats", "lb_status", "lb_ds_pack", "lb_ds_forward",
-              "lb_ds_train_forward", "lb_ds_pack_backward", "lb_ds_train_backward"):
+              "lb_ds_train_forward", "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax",
+              "lb_replay_add"):
         getattr(L, f).restype = C.c_int
     v = L.lb_abi_version()
     if v != ABI_VERSION:
@@ -120,4 +123,4 @@ def check(rc):
 EXPORTED_SYMBOLS = ("lb_abi_version", "lb_last_error", "lb_validate_config", "lb_state_bytes",
                     "lb_init", "lb_reset", "lb_step", "lb_policy", "lb_get_field", "lb_get_stats",
                     "lb_status", "lb_ds_pack", "lb_ds_forward", "lb_ds_train_forward",
-                    "lb_ds_pack_backward", "lb_ds_train_backward")
+                    "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax", "lb_replay_add")

@@ -21,7 +21,7 @@ import torch
 import torch.nn.functional as F
 from torch import optim
 
-from . import fused
+from . import _native, fused
 from .deepsets import DQNDeepSetAgent, HUGE_NEG, allreduce_gradients
 
 
@@ -47,6 +47,8 @@ class DeviceReplayBuffer:
         self.dones = torch.zeros((self.size, num_envs), device=device)
         self.pos, self.full = 0, False
         self.pos_t = torch.zeros(1, dtype=torch.long, device=device)
+        # lb_replay_add's slot words: the launch reads pp[parity], writes pp[1 - parity]
+        self.pos_pp = torch.zeros(2, dtype=torch.long, device=device)
         self.gen = generator
 
     def add_device(self, obs, next_obs, actions, rewards, dones):
@@ -58,6 +60,18 @@ class DeviceReplayBuffer:
         self.rewards.index_copy_(0, i, rewards[None])
         self.dones.index_copy_(0, i, dones[None])
         self.pos_t.add_(1).remainder_(self.size)
+
+    def add_fused(self, obs, next_obs, actions_i32, rewards, done_u8, ep_stats, ep_sum, ep_cnt, parity):
+        """add_device + obs <- next_obs + per-env finished-episode sums as ONE launch
+        (lb_replay_add); the device slot lives in pos_pp[parity] and moves to the other word."""
+        B = self.n_envs
+        pp = self.pos_pp.data_ptr()
+        _native.check(_native.lib().lb_replay_add(
+            B, int(obs[0].numel()), self.size, pp + 8 * parity, pp + 8 * (1 - parity), obs.data_ptr(),
+            next_obs.data_ptr(), actions_i32.data_ptr(), rewards.data_ptr(), done_u8.data_ptr(),
+            ep_stats.data_ptr(), self.obs.data_ptr(), self.next_obs.data_ptr(), self.actions.data_ptr(),
+            self.rewards.data_ptr(), self.dones.data_ptr(), ep_sum.data_ptr(), ep_cnt.data_ptr(),
+            torch.cuda.current_stream(obs.device).cuda_stream))
 
     def advance_host(self):
         self.pos += 1
@@ -71,6 +85,7 @@ class DeviceReplayBuffer:
     def clear(self):
         self.pos, self.full = 0, False
         self.pos_t.zero_()
+        self.pos_pp.zero_()
 
     def sample(self, batch_size):
         upper = self.size if self.full else self.pos
@@ -122,11 +137,16 @@ class DQN_DeepSets:
         self._rew = torch.zeros(self.num_envs, device=self.device)
         self._next_obs = torch.zeros((self.num_envs,) + tuple(env.observation_space.shape), device=self.device)
         self.episode_returns = []
-        self._ep_sum = torch.zeros((), dtype=torch.float64, device=self.device)
-        self._ep_cnt = torch.zeros((), dtype=torch.float64, device=self.device)
+        # per-env finished-episode sums (reduced when flushed)
+        self._ep_sum = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
+        self._ep_cnt = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
         self.train_steps = 0
-        # static buffers of the captured vector step (HIP graphs on a GPU; eager otherwise)
+        # static buffers of the captured vector step (HIP graphs on a GPU; eager otherwise).
+        # On a GPU a vector step is 4-5 launches: [pack + Q forward with the masked argmax
+        # fused | the env's random policy], the env step, and lb_replay_add (replay write,
+        # obs <- next obs, episode sums), whose slot word alternates between two graphs.
         self.use_graphs = self.device.type == "cuda"
+        self._parity = 0
         self._graph = None
         self._q = torch.zeros((self.num_envs, env.observation_space.shape[0]), device=self.device)
         self._qfrag = fused.frag_buffer(self.device) if self.use_graphs else None
@@ -145,44 +165,47 @@ class DQN_DeepSets:
         (:808-821), so this is a uniform action: the env's Philox draw (D_ACT)."""
         return self.env.policy("random", out=self._act)
 
-    def _vector_step(self, obs, masks, explore):
-        """One vector step on the device: actions, fused env step, episode-return
-        accumulators, replay write, obs <- next obs.  No host sync; graph-capturable."""
+    def _vector_step(self, obs, masks, explore, parity=0):
+        """One vector step on the device: actions, fused env step, replay write, episode
+        sums, obs <- next obs.  No host sync; graph-capturable."""
         env = self.env
         if explore:
             self._explore_actions(masks)
+        elif self.use_graphs:
+            fused.q_argmax_graphable(self.q_network, obs, masks, self._act, self._qfrag)
         else:
             with torch.no_grad():
-                if self.use_graphs:
-                    q = fused.q_forward_graphable(self.q_network, obs, self._q, self._qfrag)
-                else:
-                    q = fused.q_forward(self.q_network, obs)
-                q = torch.where(masks, q, torch.full((), HUGE_NEG, device=obs.device))
+                q = torch.where(masks, fused.q_forward(self.q_network, obs), torch.full((), HUGE_NEG, device=obs.device))
                 self._act.copy_(torch.argmax(q, dim=1))
         env.step_device(self._act, obs_out=self._next_obs, reward_out=self._rew, done_out=self._done_u8)
+        if self.use_graphs:
+            self.rb.add_fused(obs, self._next_obs, self._act, self._rew, self._done_u8, env.ep_stats,
+                              self._ep_sum, self._ep_cnt, parity)
+            return
         dones = self._done_u8.float()
-        # finished-episode returns accumulate on the device (no per-step host sync)
-        self._ep_sum += (env.ep_stats[:, 0] * dones).sum()
-        self._ep_cnt += dones.sum()
+        self._ep_sum += env.ep_stats[:, 0] * dones
+        self._ep_cnt += dones
         self.rb.add_device(obs, self._next_obs, self._act, self._rew, dones)
         obs.copy_(self._next_obs)
 
     def _build_graphs(self, obs, masks):
-        """Both vector-step variants captured once as HIP graphs: a vector step is ~20
-        small launches, replayed as one graph without the per-launch host cost.  The
-        warm-up steps run on a side stream before capture; the caller resets afterwards."""
+        """The four vector-step variants (explore or not, slot word 0 or 1) captured once as
+        HIP graphs.  The warm-up steps run on a side stream before capture; the caller
+        resets afterwards."""
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
             for explore in (False, True):
-                self._vector_step(obs, masks, explore)
+                for parity in (0, 1):
+                    self._vector_step(obs, masks, explore, parity)
         torch.cuda.current_stream(self.device).wait_stream(side)
         graphs = {}
         for explore in (False, True):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._vector_step(obs, masks, explore)
-            graphs[explore] = g
+            for parity in (0, 1):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._vector_step(obs, masks, explore, parity)
+                graphs[explore, parity] = g
         return graphs
 
     def train_step(self, global_step):
@@ -213,6 +236,7 @@ class DQN_DeepSets:
                 env.reset()
                 obs.copy_(env.obs)
                 self.rb.clear()
+                self._parity = 0
                 self._ep_sum.zero_()
                 self._ep_cnt.zero_()
             graphs = self._graph
@@ -221,9 +245,10 @@ class DQN_DeepSets:
             eps = linear_schedule(self.start_e, self.end_e, self.exploration_fraction * total_timesteps, global_step)
             explore = random.random() < eps  # one draw decides exploration for every env (:127)
             if graphs is not None:
-                graphs[explore].replay()
+                graphs[explore, self._parity].replay()
             else:
-                self._vector_step(obs, masks, explore)
+                self._vector_step(obs, masks, explore, self._parity)
+            self._parity ^= 1
             self.rb.advance_host()
             if global_step > self.learning_starts and global_step % self.train_frequency == 0:
                 loss = self.train_step(global_step)
@@ -235,9 +260,9 @@ class DQN_DeepSets:
         return self
 
     def _flush_returns(self):
-        n = float(self._ep_cnt.item())
+        n = float(self._ep_cnt.sum().item())
         if n > 0:
-            self.episode_returns.append(float(self._ep_sum.item()) / n)
+            self.episode_returns.append(float(self._ep_sum.sum().item()) / n)
         self._ep_sum.zero_()
         self._ep_cnt.zero_()
 

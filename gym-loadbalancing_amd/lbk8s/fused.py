@@ -141,3 +141,26 @@ def q_forward_graphable(qnet, x, out, frag):
     del keep
     _launch(frag, x, out, None)
     return out
+
+
+@torch.no_grad()
+def q_argmax_graphable(qnet, x, masks, actions_out, frag, q_out=None):
+    """Greedy actions of a DQNDeepSetAgent (dqn_deepset.py:134-142: argmax of the Q values
+    with invalid actions at -1e8, first index on ties) into `actions_out` (B,) int32, in two
+    launches on fixed buffers (pack into `frag`, then the forward with the argmax fused:
+    lb_ds_q_argmax), so the pair can be captured in a HIP graph.  masks: (B, R) bool or None."""
+    net = qnet.q_network.net
+    if not _geometry_ok(net, x):
+        raise RuntimeError(f"fused deep-sets forward does not cover input {tuple(x.shape)} on {x.device}")
+    if masks is not None and (masks.dtype != torch.bool or tuple(masks.shape) != tuple(x.shape[:2])
+                              or not masks.is_contiguous()):
+        raise ValueError("masks must be a contiguous (B, R) bool tensor")
+    w, keep = _weights_struct(net, None)
+    L = _native.lib()
+    stream = torch.cuda.current_stream(x.device).cuda_stream
+    _native.check(L.lb_ds_pack(C.byref(w), frag.data_ptr(), stream))
+    del keep
+    B, R, _ = x.shape
+    _native.check(L.lb_ds_q_argmax(frag.data_ptr(), x.data_ptr(), B, R, _ptr(masks), _ptr(q_out),
+                                   actions_out.data_ptr(), stream))
+    return actions_out

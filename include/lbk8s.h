@@ -196,6 +196,23 @@ int lb_ds_pack(const lb_ds_weights* w, float* frag_out, void* stream);
 int lb_ds_forward(const float* frag, const float* obs, int64_t num_envs, int32_t num_elements,
                   float* logits_out, float* value_out, void* stream);
 
+/* Greedy action of the Q network (dqn_deepset.py:134-142): actions_out[b] = first
+ * argmax over r of (masks[b][r] ? Q[b][r] : -1e8), Q from an actor-only image (lb_ds_pack
+ * with NULL critic pointers); masks [B,R] u8 or NULL (all valid); q_out [B,R] or NULL. */
+int lb_ds_q_argmax(const float* frag, const float* obs, int64_t num_envs, int32_t num_elements,
+                   const uint8_t* masks, float* q_out, int32_t* actions_out, void* stream);
+
+/* GPU-resident replay add (dqn_deepset.py:158-174, SB3 ReplayBuffer layout [slots][B]...)
+ * plus obs <- next_obs and per-env finished-episode sums, in one launch.  The slot is
+ * *pos_in (device); (pos + 1) % slots is written to *pos_out, which must be a different
+ * word (alternate two).  obs / next_obs [B, obs_floats] f32, obs_floats % 4 == 0;
+ * ep_stats/ep_sum/ep_cnt may all be NULL. */
+int lb_replay_add(int64_t num_envs, int32_t obs_floats, int64_t slots, const int64_t* pos_in, int64_t* pos_out,
+                  float* obs, const float* next_obs, const int32_t* actions, const float* reward,
+                  const uint8_t* done, const double* ep_stats, float* rb_obs, float* rb_next_obs,
+                  int64_t* rb_actions, float* rb_rewards, float* rb_dones, double* ep_sum, double* ep_cnt,
+                  void* stream);
+
 /* ---- Fused deep-sets training -----------------------------
  * Replaces the reference's autograd through the same modules in the PPO update
  * (envs/ppo_deepset.py:227-263 -> deep_sets_agent_original.py:56-106).  The training

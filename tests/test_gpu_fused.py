@@ -104,3 +104,64 @@ def test_fused_rejects_uncovered_inputs():
     logits, value = fused.deepsets_forward(agent, x)  # torch modules on the same device
     assert logits.shape == (4, 81) and value.shape == (4,) and logits.is_cuda
     np.testing.assert_array_equal(np.isfinite(logits.cpu().numpy()), True)
+
+
+@pytest.mark.parametrize("R", [7, 9, 20, 65])
+def test_fused_q_argmax(R):
+    """lb_ds_q_argmax: the Q forward with the masked greedy action fused
+    (dqn_deepset.py:134-142: argmax of where(mask, q, -1e8), first index on ties)."""
+    from lbk8s import fused
+    from lbk8s.deepsets import DQNDeepSetAgent
+    torch.manual_seed(40 + R)
+    q = DQNDeepSetAgent(8).cuda()
+    B = 1001
+    x = torch.randn(B, R, 8, device="cuda") * 2
+    x[5] = x[5, :1]  # every row equal: Q ties on the whole set -> action 0
+    masks = torch.rand(B, R, device="cuda") > 0.3
+    masks[7] = False  # nothing valid: every entry -1e8 -> action 0
+    masks[5] = True
+    frag = fused.frag_buffer("cuda")
+    act = torch.empty(B, dtype=torch.int32, device="cuda")
+    qv = torch.empty(B, R, device="cuda")
+    fused.q_argmax_graphable(q, x, masks, act, frag, q_out=qv)
+    with torch.no_grad():
+        near(qv, q.q_network(x), what=f"q R={R}")
+    expect = torch.where(masks, qv, torch.full((), -1e8, device="cuda")).argmax(1)
+    assert torch.equal(act.long(), expect)
+    assert int(act[5]) == 0 and int(act[7]) == 0
+    fused.q_argmax_graphable(q, x, None, act, frag)
+    assert torch.equal(act.long(), qv.argmax(1))
+
+
+def test_replay_add_matches_torch():
+    """lb_replay_add == the torch replay add (DeviceReplayBuffer.add_device) + obs <- next_obs
+    + per-env finished-episode sums, with the slot word alternating."""
+    from lbk8s.dqn import DeviceReplayBuffer
+    torch.manual_seed(0)
+    B, R, slots = 300, 9, 4
+    g = torch.Generator(device="cuda")
+    a = DeviceReplayBuffer(slots * B, B, (R, 8), "cuda", g)
+    b = DeviceReplayBuffer(slots * B, B, (R, 8), "cuda", g)
+    obs_a = torch.randn(B, R, 8, device="cuda")
+    obs_b = obs_a.clone()
+    es_a = torch.zeros(B, dtype=torch.float64, device="cuda")
+    ec_a = torch.zeros_like(es_a)
+    es_b, ec_b = es_a.clone(), ec_a.clone()
+    for step in range(slots + 2):  # wraps around
+        nxt = torch.randn(B, R, 8, device="cuda")
+        act = torch.randint(0, R, (B,), dtype=torch.int32, device="cuda")
+        rew = torch.randn(B, device="cuda")
+        done = (torch.rand(B, device="cuda") < 0.3).to(torch.uint8)
+        ep = torch.randn(B, 16, dtype=torch.float64, device="cuda")
+        a.add_fused(obs_a, nxt, act, rew, done, ep, es_a, ec_a, step % 2)
+        d = done.double()
+        es_b += ep[:, 0] * d
+        ec_b += d
+        b.add_device(obs_b, nxt, act, rew, done.float())
+        obs_b.copy_(nxt)
+    torch.cuda.synchronize()
+    for f in ("obs", "next_obs", "actions", "rewards", "dones"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    assert torch.equal(obs_a, obs_b)
+    assert torch.equal(ec_a, ec_b) and torch.allclose(es_a, es_b, rtol=0, atol=1e-12)
+    assert int(a.pos_pp[(slots + 2) % 2]) == int(b.pos_t) == (slots + 2) % slots
