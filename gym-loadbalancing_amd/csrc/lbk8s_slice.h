@@ -96,6 +96,10 @@ struct SEnv {
 };
 
 // get_state() (:688-758): rows [zone, zone_cpu_cap, cpu, topo_lat, lat, req_zone, thr, dt]
+#ifdef LB_ABL_SLICE_ROWS
+// (ablation: each lane stores its own 32-byte rows as two 16-byte halves; a store
+// instruction then covers every other 16 bytes and the nontemporal halves reach HBM as
+// partial writes: 2,947 B written per env-step at E = 64 instead of ~2,190)
 template <int W, int EPL>
 __device__ __forceinline__ void slice_write_obs(const Params& p, float* out, int64_t env, int lane,
                                                 const SEnv<EPL>& v) {
@@ -120,6 +124,46 @@ __device__ __forceinline__ void slice_write_obs(const Params& p, float* out, int
         st_stream(row + 1, make_float4(-1.f, rz, thr, dt));
     }
 }
+#else
+// The env's R x 32-byte block is written as contiguous runs: store c covers float4s
+// cW .. cW + W - 1 of the block (rows cW/2 .. cW/2 + W/2 - 1), lane l the float4 2r + h of
+// row r = cW/2 + (l >> 1), h = l & 1.  Row r < E is endpoint r, held by lane r % W in
+// slot r / W = c >> 1, so each lane's halves come from lane (c & 1) W/2 + (l >> 1) by a
+// lane shuffle; the reject row (r = E) is the same on every lane.
+template <int W, int EPL>
+__device__ __forceinline__ void slice_write_obs(const Params& p, float* out, int64_t env, int lane,
+                                                const SEnv<EPL>& v) {
+    float4* base = reinterpret_cast<float4*>(out + env * (int64_t)p.R * 8);
+    const float rz = (float)v.s.rz, thr = (float)threshold(v.s.thr_idx), dt = (float)v.dt;
+    const int n4 = 2 * p.R, h = lane & 1;
+#pragma unroll
+    for (int k = 0; k <= EPL; ++k) {
+        // this lane's endpoint of slot k (garbage-free zeros past the valid range)
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+        if (k < EPL) {
+            const int z = em_zone(v.em[k]);
+            a = make_float4((float)z, (float)zcap_val(v.zcap, z), v.ocpu[k], (float)topo_val(v.topo, z, v.s.rz));
+            b = make_float4(v.olat[k], rz, thr, dt);
+        }
+#pragma unroll
+        for (int c = 2 * k; c < 2 * k + 2; ++c) {
+            if (c * W >= n4) continue;           // uniform over the env's lanes
+            const int q = c * W + lane;          // float4 index inside the env's block
+            const int r = q >> 1;                // row
+            // shuffles with every lane of the slice active (a source lane must not be masked)
+            const int src = (c & 1) * (W / 2) + (lane >> 1);
+            const float4 sa = make_float4(__shfl(a.x, src, W), __shfl(a.y, src, W), __shfl(a.z, src, W),
+                                          __shfl(a.w, src, W));
+            const float4 sb = make_float4(__shfl(b.x, src, W), __shfl(b.y, src, W), __shfl(b.z, src, W),
+                                          __shfl(b.w, src, W));
+            // rows past E: the reject row (r == E, present iff R > E); later rows are past R
+            const float4 o = (r < p.E && k < EPL) ? (h ? sb : sa)
+                                                  : (h ? make_float4(-1.f, rz, thr, dt) : make_float4(-1.f, -1.f, -1.f, -1.f));
+            if (q < n4) st_stream(base + q, o);
+        }
+    }
+}
+#endif
 
 // Philox mode: the lane's endpoints of the episode (reset() :328, :379-386) drawn again
 // instead of loaded (the draws are a pure function of seed, env id and episode)
