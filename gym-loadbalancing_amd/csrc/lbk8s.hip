@@ -659,6 +659,21 @@ int lb_ds_train_forward(const float* frag, const float* obs, int64_t num_envs, i
     return check_launch();
 }
 
+int lb_ppo_head(const float* logits, const uint8_t* masks, const float* actions, const float* oldlogp,
+                const float* adv, const float* ret, const float* vold, const float* value, int64_t num_sets,
+                int32_t num_elements, float clip_coef, float ent_coef, float vf_coef, int32_t clip_vloss,
+                float* dlogits, float* dvalue, float* terms, void* stream) {
+    if (!logits || !actions || !oldlogp || !adv || !ret || !vold || !value || !dlogits || !dvalue || !terms ||
+        num_sets < 1)
+        return fail("ppo head buffers NULL or num_sets < 1");
+    if (num_elements < 1 || num_elements > 128) return fail("num_elements must be in [1, 128]");
+    PPOHeadParams p{logits, masks, actions, oldlogp, adv, ret, vold, value, dlogits, dvalue, terms,
+                    num_sets, num_elements, clip_coef, ent_coef, vf_coef, 1.0f / (float)num_sets, clip_vloss};
+    const unsigned grid = (unsigned)std::min<int64_t>((num_sets + 3) / 4, 8192);
+    hipLaunchKernelGGL(k_ppo_head, dim3(grid), dim3(256), 0, (hipStream_t)stream, p);
+    return check_launch();
+}
+
 int lb_ds_pack_backward(const lb_ds_weights* w, float* bwd_frag_out, void* stream) {
     static_assert(DSB_FLOATS == LB_DS_BWD_FLOATS, "backward image layout and header disagree");
     if (!w || !bwd_frag_out) return fail("weights/bwd_frag_out NULL");

@@ -456,6 +456,101 @@ __global__ __launch_bounds__(DSR_COLS * DSR_GROUPS) void k_ds_wgrad_reduce(const
     }
 }
 
+// PPO loss head (envs/ppo_deepset.py:227-263 on a minibatch): per set, from the logits
+// and the value, the clipped policy loss, the (clipped) value loss, the Categorical
+// entropy, approx_kl and clipfrac terms, and the loss's gradient w.r.t. every logit and the
+// value — autograd's tie rules included (torch.max of two tensors splits the gradient
+// evenly on ties; clamp passes it on the closed interval; masked logits are -1e8 and get
+// none).  One wave per set, rows r and r + 64 on lane r.  adv: already normalised.
+struct PPOHeadParams {
+    const float* logits;    // [M][R]
+    const uint8_t* masks;   // [M][R] or NULL
+    const float* actions;   // [M] (float, as PPO's storage keeps them)
+    const float* oldlogp;   // [M]
+    const float* adv;       // [M]
+    const float* ret;       // [M]
+    const float* vold;      // [M]
+    const float* value;     // [M]
+    float* dlogits;         // [M][R]
+    float* dvalue;          // [M]
+    float* terms;           // [M][6]: pg, max(v terms), entropy, kl, clipped, loss
+    int64_t M;
+    int R;
+    float clip, ent_coef, vf_coef, inv_m;
+    int clip_vloss;
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_ppo_head(PPOHeadParams p) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
+    const int R = p.R;
+    for (int64_t s = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); s < p.M; s += nw) {
+        const float* lg = p.logits + s * R;
+        const int r0 = lane, r1 = lane + 64;
+        const bool v0 = r0 < R, v1 = r1 < R;
+        const bool m0 = v0 && (!p.masks || p.masks[s * R + r0]);
+        const bool m1 = v1 && (!p.masks || p.masks[s * R + r1]);
+        const float l0 = v0 ? (m0 ? lg[r0] : -1e8f) : -INFINITY;
+        const float l1 = v1 ? (m1 ? lg[r1] : -1e8f) : -INFINITY;
+        const float mx = wave_max(fmaxf(l0, l1));
+        const float e0 = v0 ? expf(l0 - mx) : 0.f, e1 = v1 ? expf(l1 - mx) : 0.f;
+        const float lse = mx + logf(wave_sum(e0 + e1));
+        const float lp0 = l0 - lse, lp1 = l1 - lse;
+        const float p0 = v0 ? expf(lp0) : 0.f, p1 = v1 ? expf(lp1) : 0.f;
+        const float H = -wave_sum((v0 ? p0 * lp0 : 0.f) + (v1 ? p1 * lp1 : 0.f));
+        const int a = (int)p.actions[s];
+        const float nlp = __shfl(a < 64 ? lp0 : lp1, a & 63);
+        const float logratio = nlp - p.oldlogp[s];
+        const float ratio = expf(logratio);
+        const float A = p.adv[s];
+        const float lo = 1.f - p.clip, hi = 1.f + p.clip;
+        const float rc = fminf(fmaxf(ratio, lo), hi);
+        const float pg1 = -A * ratio, pg2 = -A * rc;
+        const float w1 = pg1 > pg2 ? 1.f : (pg1 == pg2 ? 0.5f : 0.f);
+        const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+        const float g_nlp = p.inv_m * (w1 * (-A) + (1.f - w1) * (-A) * inr) * ratio;
+        const float ge = p.ent_coef * p.inv_m;
+        if (v0) p.dlogits[s * R + r0] = m0 ? g_nlp * ((r0 == a ? 1.f : 0.f) - p0) + ge * p0 * (lp0 + H) : 0.f;
+        if (v1) p.dlogits[s * R + r1] = m1 ? g_nlp * ((r1 == a ? 1.f : 0.f) - p1) + ge * p1 * (lp1 + H) : 0.f;
+        if (lane == 0) {
+            const float v = p.value[s], rt = p.ret[s], vo = p.vold[s];
+            const float vu = (v - rt) * (v - rt);
+            float vt = vu, gv;
+            if (p.clip_vloss) {
+                const float d = v - vo;
+                const float vc = vo + fminf(fmaxf(d, -p.clip), p.clip);
+                const float vcl = (vc - rt) * (vc - rt);
+                vt = fmaxf(vu, vcl);
+                const float wu = vu > vcl ? 1.f : (vu == vcl ? 0.5f : 0.f);
+                const float inv = (d >= -p.clip && d <= p.clip) ? 1.f : 0.f;
+                gv = wu * 2.f * (v - rt) + (1.f - wu) * 2.f * (vc - rt) * inv;
+            } else {
+                gv = 2.f * (v - rt);
+            }
+            p.dvalue[s] = p.vf_coef * 0.5f * p.inv_m * gv;
+            const float pgt = fmaxf(pg1, pg2);
+            float* t = p.terms + s * 6;
+            t[0] = pgt;
+            t[1] = vt;
+            t[2] = H;
+            t[3] = (ratio - 1.f) - logratio;
+            t[4] = fabsf(ratio - 1.f) > p.clip ? 1.f : 0.f;
+            t[5] = pgt - p.ent_coef * H + p.vf_coef * 0.5f * vt;
+        }
+    }
+}
+
 // lb_ds_pack_backward: one thread per image float; transposed fragment order for the
 // 64x64 matrices (lane l of fragment (nt, k) holds W^T[16nt + (l & 15)][in(k, l >> 4)])
 __global__ void k_ds_pack_bwd(lb_ds_weights w, float* out) {

@@ -94,6 +94,8 @@ def lib():
     L.lb_ds_pack.argtypes = [C.POINTER(LBDSWeightsC), vp, vp]
     L.lb_ds_forward.argtypes = [vp, vp, i64, i32, vp, vp, vp]
     L.lb_ds_q_argmax.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp]
+    f32 = C.c_float
+    L.lb_ppo_head.argtypes = [vp] * 8 + [i64, i32, f32, f32, f32, i32, vp, vp, vp, vp]
     L.lb_replay_add.argtypes = [i64, i32, i64] + [vp] * 15 + [vp]
     L.lb_ds_train_forward.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp]
     L.lb_ds_pack_backward.argtypes = [C.POINTER(LBDSWeightsC), vp, vp]
@@ -101,7 +103,7 @@ def lib():
     for f in ("lb_validate_config", "lb_state_bytes", "lb_init", "lb_reset", "lb_step", "lb_policy",
               "lb_get_field", "lb_get_stats", "lb_status", "lb_ds_pack", "lb_ds_forward",
               "lb_ds_train_forward", "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax",
-              "lb_replay_add"):
+              "lb_replay_add", "lb_ppo_head"):
         getattr(L, f).restype = C.c_int
     v = L.lb_abi_version()
     if v != ABI_VERSION:
@@ -123,4 +125,4 @@ def check(rc):
 EXPORTED_SYMBOLS = ("lb_abi_version", "lb_last_error", "lb_validate_config", "lb_state_bytes",
                     "lb_init", "lb_reset", "lb_step", "lb_policy", "lb_get_field", "lb_get_stats",
                     "lb_status", "lb_ds_pack", "lb_ds_forward", "lb_ds_train_forward",
-                    "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax", "lb_replay_add")
+                    "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax", "lb_replay_add", "lb_ppo_head")

@@ -190,3 +190,46 @@ def actor_only(owner, actor_net, x):
     """EquivariantDeepSet training forward (the DQN Q network): logits (B, R)."""
     x = x.float().contiguous()
     return _FusedDeepSetsTrain.apply(x, owner, actor_net, None, *_eq_params(actor_net))
+
+
+class _PPOHead(torch.autograd.Function):
+    """ppo_deepset.py:227-263's loss from (logits, value) in one launch (lb_ppo_head): the
+    per-set terms and the loss's gradient w.r.t. logits and value, which backward returns
+    (scaled by the incoming gradient of the loss).  Returns (loss, stats) with stats =
+    (pg_loss, mean value term, entropy, approx_kl, clipfrac), not differentiable."""
+
+    @staticmethod
+    def forward(ctx, logits, value, masks, actions, oldlogp, adv, ret, vold, clip, ent_coef, vf_coef, clip_vloss):
+        M, R = logits.shape
+        dev = logits.device
+        logits = logits.float().contiguous()
+        dlogits = torch.empty_like(logits)
+        dvalue = torch.empty((M,), dtype=torch.float32, device=dev)
+        terms = torch.empty((M, 6), dtype=torch.float32, device=dev)
+        c = lambda t: t.float().contiguous()  # noqa: E731
+        m = None
+        if masks is not None:
+            if masks.dtype != torch.bool or tuple(masks.shape) != (M, R):
+                raise ValueError("masks must be (M, R) bool")
+            m = masks.contiguous()
+        keep = [c(actions), c(oldlogp), c(adv), c(ret), c(vold), c(value.reshape(-1))]
+        _native.check(_native.lib().lb_ppo_head(
+            logits.data_ptr(), fused._ptr(m), *[t.data_ptr() for t in keep], M, R, float(clip), float(ent_coef),
+            float(vf_coef), int(bool(clip_vloss)), dlogits.data_ptr(), dvalue.data_ptr(), terms.data_ptr(),
+            _stream(dev)))
+        means = terms.mean(0)
+        ctx.save_for_backward(dlogits, dvalue)
+        ctx.vshape = value.shape
+        stats = means[:5]
+        ctx.mark_non_differentiable(stats)
+        return means[5], stats
+
+    @staticmethod
+    def backward(ctx, gloss, gstats):
+        dlogits, dvalue = ctx.saved_tensors
+        return (dlogits * gloss, (dvalue * gloss).view(ctx.vshape)) + (None,) * 10
+
+
+def ppo_head(logits, value, masks, actions, oldlogp, adv, ret, vold, clip_coef, ent_coef, vf_coef, clip_vloss):
+    return _PPOHead.apply(logits, value, masks, actions, oldlogp, adv, ret, vold, clip_coef, ent_coef, vf_coef,
+                          clip_vloss)

@@ -29,7 +29,21 @@ from .deepsets import DeepSetAgent, allreduce_gradients
 
 def ppo_loss(agent, obs, actions, logprobs_old, masks, advantages, returns, values_old,
              clip_coef=0.2, ent_coef=0.01, vf_coef=0.5, norm_adv=True, clip_vloss=True):
-    """One minibatch of ppo_deepset.py:227-263 -> (loss, pg_loss, v_loss, entropy, approx_kl, clipfrac)."""
+    """One minibatch of ppo_deepset.py:227-263 -> (loss, pg_loss, v_loss, entropy, approx_kl, clipfrac).
+
+    On a HIP device the deep-sets forward/backward are the fused training kernels and the
+    loss head (log-softmax, ratio, clipped losses, entropy and their gradients) is one
+    launch (fused_train.ppo_head); elsewhere, the same ops as the reference in torch."""
+    from . import fused_train
+    if (obs.is_cuda and torch.is_grad_enabled() and fused_train.supported(agent.actor.net, obs)
+            and (masks is None or masks.shape[-1] == obs.shape[1])):
+        logits, newvalue = agent.actor_critic(obs)
+        adv = advantages
+        if norm_adv:
+            adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+        loss, st = fused_train.ppo_head(logits, newvalue.view(-1), masks, actions, logprobs_old, adv, returns,
+                                        values_old, clip_coef, ent_coef, vf_coef, clip_vloss)
+        return loss, st[0], 0.5 * st[1], st[2], st[3], st[4]
     # the same Categorical ops as the reference: the actor's last Gamma term shifts every
     # logit of a set equally, so its true gradient is 0 and what autograd returns is
     # rounding noise that only an identical op sequence reproduces

@@ -249,6 +249,17 @@ int lb_ds_train_forward(const float* frag, const float* obs, int64_t num_envs, i
                         float* logits_out, float* psi_mean_out, float* save_actor, float* save_critic,
                         void* stream);
 
+/* PPO loss head (envs/ppo_deepset.py:227-263) for M sets of R <= 128 elements: per-set
+ * terms [M,6] (policy term max(pg1, pg2), value term, entropy, approx-kl term, clipped
+ * indicator, loss term = pg - ent_coef H + vf_coef/2 v; their means are the reference's
+ * logged scalars and loss) and the loss's gradient w.r.t. logits [M,R] and value [M],
+ * with autograd's tie rules (an even split between equal max operands, clamp's closed
+ * interval).  masks [M,R] u8 or NULL; actions as float; adv already normalised. */
+int lb_ppo_head(const float* logits, const uint8_t* masks, const float* actions, const float* oldlogp,
+                const float* adv, const float* ret, const float* vold, const float* value, int64_t num_sets,
+                int32_t num_elements, float clip_coef, float ent_coef, float vf_coef, int32_t clip_vloss,
+                float* dlogits, float* dvalue, float* terms, void* stream);
+
 /* Pack the backward image [LB_DS_BWD_FLOATS] (transposed layer-2/3 matrices). */
 int lb_ds_pack_backward(const lb_ds_weights* w, float* bwd_frag_out, void* stream);
 

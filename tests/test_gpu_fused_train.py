@@ -120,3 +120,57 @@ def test_train_forward_caches_follow_updates():
         opt_r.step()
     for (name, p), (_, q) in zip(agent.named_parameters(), ref.named_parameters()):
         _check(p, q, f"param {name}", 1e-4, 1e-5)
+
+
+@pytest.mark.parametrize("R,masked", [(9, False), (65, True), (80, True)])
+def test_ppo_head_matches_autograd(R, masked):
+    """lb_ppo_head (loss terms and d loss / d logits, d loss / d value) against autograd
+    through ppo_deepset.py:227-263's ops in float64 (the reference's formulation: masked
+    Categorical, clipped ratio, clipped value loss, entropy bonus)."""
+    from torch.distributions import Categorical
+    from lbk8s import fused_train
+    g = torch.Generator().manual_seed(R)
+    M = 3001
+    logits = torch.randn(M, R, generator=g) * 3
+    masks = torch.rand(M, R, generator=g) > 0.2 if masked else torch.ones(M, R, dtype=torch.bool)
+    actions = torch.randint(0, R, (M,), generator=g).float()
+    masks[torch.arange(M), actions.long()] = True  # the taken action is valid (ratio ~ 1, not exp(1e8))
+    value = torch.randn(M, generator=g) * 5
+    ret = value + torch.randn(M, generator=g) * 2
+    vold = value + torch.randn(M, generator=g) * 0.3      # |v - vold| on both sides of clip
+    adv = torch.randn(M, generator=g)
+    with torch.no_grad():  # old log-probs around the new ones: ratios in and out of [0.8, 1.2]
+        lp = torch.log_softmax(torch.where(masks, logits, torch.full((), -1e8)), 1)
+        oldlogp = lp.gather(1, actions.long()[:, None]).squeeze(1) + torch.randn(M, generator=g) * 0.3
+    clip, ent_c, vf_c = 0.2, 0.01, 0.5
+
+    L = logits.double().requires_grad_()
+    V = value.double().requires_grad_()
+    dist = Categorical(logits=torch.where(masks, L, torch.full((), -1e8, dtype=torch.float64)))
+    nlp = dist.log_prob(actions.long())
+    logratio = nlp - oldlogp.double()
+    ratio = logratio.exp()
+    A = adv.double()
+    pg = torch.max(-A * ratio, -A * torch.clamp(ratio, 1 - clip, 1 + clip)).mean()
+    vu = (V - ret.double()) ** 2
+    vc = vold.double() + torch.clamp(V - vold.double(), -clip, clip)
+    vl = 0.5 * torch.max(vu, (vc - ret.double()) ** 2).mean()
+    ent = dist.entropy().mean()
+    loss = pg - ent_c * ent + vl * vf_c
+    loss.backward()
+
+    Lg = logits.cuda().requires_grad_()
+    Vg = value.cuda().requires_grad_()
+    gl, st = fused_train.ppo_head(Lg, Vg, masks.cuda(), actions.cuda(), oldlogp.cuda(), adv.cuda(), ret.cuda(),
+                                  vold.cuda(), clip, ent_c, vf_c, True)
+    gl.backward()
+    close(gl, loss.item(), rtol=1e-5, atol=1e-6, what="loss")
+    close(st[0], pg.item(), rtol=1e-5, atol=1e-6, what="pg_loss")
+    close(0.5 * st[1], vl.item(), rtol=1e-5, atol=1e-6, what="v_loss")
+    close(st[2], ent.item(), rtol=1e-5, atol=1e-6, what="entropy")
+    kl = ((ratio - 1) - logratio).mean().item()
+    close(st[3], kl, rtol=1e-4, atol=1e-6, what="approx_kl")
+    cf = ((ratio - 1).abs() > clip).double().mean().item()
+    assert abs(float(st[4]) - cf) <= 2.0 / M, "clipfrac"
+    _check(Lg.grad, L.grad, "d loss / d logits", 1e-4, 1e-5)
+    _check(Vg.grad, V.grad, "d loss / d value", 1e-4, 1e-6)
