@@ -143,8 +143,7 @@ __global__ void k_policy(Params p, int kind, int32_t* out) {
     if (env >= p.B) return;
     const Scal s = sc_unpack(p.sc[env]);
     if (kind == LB_POLICY_RANDOM) {
-        U4 w = draw(p, env, (uint32_t)(p.acc3[env] >> 32), (uint32_t)s.step, D_ACT);
-        out[env] = (int32_t)bounded(w.x, (uint32_t)p.A);
+        out[env] = random_action(p, env, p.acc3[env], s.step);
         return;
     }
     const int nf = p.A - 1;
@@ -482,8 +481,9 @@ int lb_step(void* state, const lb_config* cfg, int64_t num_envs, const int32_t* 
             float* obs_out, float* reward_out, uint8_t* done_out, float* terminal_obs_out,
             double* ep_stats_out, const lb_trace* trace, void* stream) {
     if (int r = validate(cfg)) return r;
-    if (!state || num_envs < 1 || !actions) return fail("state/actions NULL or num_envs < 1");
+    if (!state || num_envs < 1) return fail("state NULL or num_envs < 1");
     const bool tr = cfg->rng_mode == LB_RNG_TRACE;
+    if (!actions && tr) return fail("actions NULL (the fused random policy) needs Philox mode");
     if (tr && (!trace || !trace->step_x1 || !trace->step_x2 || !trace->step_r || !trace->step_n))
         return fail("trace mode: lb_step needs trace->step_* arrays");
     if (tr && cfg->auto_reset &&

@@ -228,6 +228,13 @@ __device__ __forceinline__ U4 draw(const Params& p, int64_t env, uint32_t episod
     return philox((uint32_t)gid, episode, slot, dom | ((uint32_t)(gid >> 32) << 8), p.key0, p.key1);
 }
 
+// the env's uniform random action for this step (action_space.sample()): lb_policy's
+// LB_POLICY_RANDOM and lb_step's fused random policy (actions == NULL) draw the same value
+__device__ __forceinline__ int32_t random_action(const Params& p, int64_t env, uint64_t acc3, uint32_t step) {
+    const U4 w = draw(p, env, (uint32_t)(acc3 >> 32), step, D_ACT);
+    return (int32_t)bounded(w.x, (uint32_t)p.A);
+}
+
 template <bool TRACE>
 __device__ __forceinline__ void node_draw(const Params& p, int64_t env, uint32_t episode, int n,
                                           int& ty, int& zo, int& cpu) {

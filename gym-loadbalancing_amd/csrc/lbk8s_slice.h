@@ -394,7 +394,7 @@ __global__ __launch_bounds__(BLOCK) LB_SLICE_OCC void k_step_slice(Params p) {
     // ---- phase 0: independent loads (state + action)
     SEnv<EPL> v;
     slice_load<W, EPL, stored>(p, env, lane, v);
-    const int a = p.actions[env];
+    const int a = p.actions ? p.actions[env] : random_action(p, env, v.acc3, v.s.step);  // fused random policy
 
     // ---- phase 1: decode, then every table lookup the step needs, issued together
     v.s.step = v.s.step < 0xFFFF ? v.s.step + 1 : 0xFFFF;

@@ -301,12 +301,13 @@ __global__ __launch_bounds__(BLOCK) void k_step_tpe(Params p) {
         }
         ed[e] = e < E ? ld_state(p.edyn + i) : 0u;
     }
-    const int a = ld_state(p.actions + ev);
+    int a = p.actions ? ld_state(p.actions + ev) : 0;
     v.t = ld_state(p.t + ev);
     v.s = sc_unpack(ld_state(p.sc + ev));
     v.zcap = ld_state(p.zcap + ev);
     v.acc2 = ld_state(p.acc2 + ev);
     v.acc3 = ld_state(p.acc3 + ev);
+    if (!p.actions) a = random_action(p, ev, v.acc3, v.s.step);  // fused random policy
     if constexpr (stored) {
         v.topo = ld_state(p.topo + ev);
         v.nz0 = ld_state(p.nzone + ev);

@@ -313,8 +313,10 @@ class LBVecEnv:
                     done_out=None, ep_stats_out=None):
         """Launch one fused step on device tensors; no host sync, no infos.
 
-        actions: (B,) int32 device tensor.  obs_out / reward_out / done_out default to the
-        env's own buffers; pass slices of a rollout ring to write there directly.
+        actions: (B,) int32 device tensor, or None: every env takes its uniform random action
+        drawn inside the step kernel (the value policy("random") would return; Philox mode).
+        obs_out / reward_out / done_out default to the env's own buffers; pass slices of a
+        rollout ring to write there directly.
         """
         if not self._reset_called:
             raise TypeError("step() called before reset()")

@@ -140,7 +140,9 @@ int lb_reset(void* state, const lb_config* cfg, int64_t num_envs, const uint8_t*
              float* obs_out, const lb_trace* trace, void* stream);
 
 /* step(action) (:403-513) for all envs.  actions [B] int32 (Python semantics:
- * -E..-1 wrap, E = reject, > E unrecognised/stale).  Outputs: obs [B,R,8] f32,
+ * -E..-1 wrap, E = reject, > E unrecognised/stale); actions == NULL (Philox mode): every
+ * env takes the uniform random action lb_policy(LB_POLICY_RANDOM) would return, drawn in
+ * the step kernel (BASELINE config 2's random policy in one launch).  Outputs: obs [B,R,8] f32,
  * reward [B] f32, done [B] u8; with cfg.auto_reset, envs that finish are reset in
  * the same launch and their pre-reset obs go to terminal_obs_out (may be NULL) and
  * their accumulators to ep_stats_out [B, LB_ST_K] f64 (may be NULL). */

@@ -146,3 +146,24 @@ def test_full_size_properties():
         a = torch.randint(0, 9, (B,), dtype=torch.int32, device="cuda", generator=gen)
         o2, _, _, _ = env2.step(a)
     assert torch.equal(o2, obs)
+
+
+@pytest.mark.parametrize("B,kw", [(4096, {}), (1 << 18, {}), (3000, dict(num_endpoints=64, reward_function="multi")),
+                                  (40000, dict(num_endpoints=20))])
+def test_fused_random_policy_step(B, kw):
+    """lb_step with actions == NULL (the env's Philox random policy drawn inside the step
+    kernel) == lb_policy(random) then lb_step, bit for bit, across auto-resets; covers the
+    thread-per-env kernel (stored and recomputed scenario) and both slice shapes."""
+    from lbk8s import LBVecEnv
+    envs = [LBVecEnv(B, seed=11, as_tensors=True, episode_length=7, **kw) for _ in range(2)]
+    for e in envs:
+        e.reset()
+    act = torch.empty(B, dtype=torch.int32, device="cuda")
+    for _ in range(16):
+        envs[0].policy("random", out=act)
+        envs[0].step_device(act)
+        envs[1].step_device(None)
+        for f in ("obs", "rewards", "dones"):
+            assert torch.equal(getattr(envs[0], f), getattr(envs[1], f)), f
+    assert torch.equal(envs[0].stats(), envs[1].stats())
+    assert envs[1].status() == 0

@@ -8,7 +8,8 @@ Prints one JSON line per (config, B): ms per step, env-steps/s, algorithmic GB/s
 --config2: 4096 default envs driven by the env's own Philox random policy (lb_policy +
 lb_step per vector step), 1,000 warm-up + 10,000 timed vector steps, launched eagerly and
 as HIP graphs of 100 vector steps each (at this size a step is a few microseconds of GPU
-time, below the cost of launching it from the host).
+time, below the cost of launching it from the host), and as graphs of lb_step with the
+random policy fused into the step kernel (actions == NULL: one launch per vector step).
 """
 import argparse
 import json
@@ -98,7 +99,18 @@ def config2(torch, LBVecEnv, dev, B=4096, warmup=1000, steps=10000, per_graph=10
     g.replay()
     graph_ms = timed(lambda n: [g.replay() for _ in range(n // per_graph)], steps)
     assert env.status() == 0
-    for mode, ms in (("eager", eager_ms), ("hip_graph", graph_ms)):
+    # the random policy fused into the step kernel (lb_step with actions == NULL)
+    def fused_step(i):
+        env.step_device(None, obs_out=ring[i % T], reward_out=rew[i % T], done_out=dn[i % T])
+
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g2):
+        for i in range(per_graph):
+            fused_step(i)
+    g2.replay()
+    fused_ms = timed(lambda n: [g2.replay() for _ in range(n // per_graph)], steps)
+    assert env.status() == 0
+    for mode, ms in (("eager", eager_ms), ("hip_graph", graph_ms), ("hip_graph_fused_policy", fused_ms)):
         print(json.dumps(dict(config="config2 default, random policy", envs=B, mode=mode, vector_steps=steps,
                               ms_per_step=round(ms / steps, 5), env_steps_per_s=B * steps / ms * 1e3)), flush=True)
 
