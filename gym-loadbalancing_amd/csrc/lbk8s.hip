@@ -230,6 +230,13 @@ struct Geo {
 // 1.00 ms per step, 4096 envs 8.9 vs 20.7 us.  Both shapes give the same EP = W * EPL
 // (the next power of two >= max(E, 16)), so the state layout does not depend on B.
 [[maybe_unused]] constexpr int64_t WIDE_SLICE_MAX_B = 32768;
+// E <= 8, few envs (config 2: 4096): 64-thread blocks, so the batch spreads over 4x more
+// CUs (every TPE kernel works per wave).  LB_ABL_TPE_BLOCK256 keeps 256-thread blocks.
+#ifdef LB_ABL_TPE_BLOCK256
+constexpr int64_t SMALL_TPE_MAX_B = 0;
+#else
+constexpr int64_t SMALL_TPE_MAX_B = 65536;
+#endif
 #if defined(LB_ABL_SPLIT_RESET) || defined(LB_ABL_SCEN_SPLIT)
 constexpr bool kSplitReset = true;
 #else
@@ -466,6 +473,12 @@ int lb_reset(void* state, const lb_config* cfg, int64_t num_envs, const uint8_t*
     Geo g = geometry(cfg, num_envs);
     hipStream_t s = (hipStream_t)stream;
     if (g.tpe) {
+        if (num_envs <= SMALL_TPE_MAX_B) {
+            const unsigned nb = (unsigned)((num_envs + 63) / 64);
+            if (tr) hipLaunchKernelGGL((k_reset_tpe<true, 64>), dim3(nb), dim3(64), 0, s, p);
+            else hipLaunchKernelGGL((k_reset_tpe<false, 64>), dim3(nb), dim3(64), 0, s, p);
+            return check_launch();
+        }
         if (tr) hipLaunchKernelGGL(k_reset_tpe<true>, dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);
         else hipLaunchKernelGGL(k_reset_tpe<false>, dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);
         return check_launch();
@@ -503,6 +516,12 @@ int lb_step(void* state, const lb_config* cfg, int64_t num_envs, const int32_t* 
     hipStream_t s = (hipStream_t)stream;
     if (g.tpe) {
         const bool recompute = kRecomputeScenario && num_envs >= SCEN_RECOMPUTE_MIN_B;
+        if (num_envs <= SMALL_TPE_MAX_B && !recompute) {
+            const unsigned nb = (unsigned)((num_envs + 63) / 64);
+            if (tr) hipLaunchKernelGGL((k_step_tpe<true, false, 64>), dim3(nb), dim3(64), 0, s, p);
+            else hipLaunchKernelGGL((k_step_tpe<false, false, 64>), dim3(nb), dim3(64), 0, s, p);
+            return check_launch();
+        }
         if (tr) hipLaunchKernelGGL((k_step_tpe<true, false>), dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);
         else if (recompute) hipLaunchKernelGGL((k_step_tpe<false, true>), dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);
         else hipLaunchKernelGGL((k_step_tpe<false, false>), dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);

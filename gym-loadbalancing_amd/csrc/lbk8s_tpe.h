@@ -250,13 +250,15 @@ __device__ __forceinline__ void tpe_store_scalars(const Params& p, int64_t env, 
     if (p.reward_fn != LB_REWARD_NAIVE) st_state(p.last_r + env, v.last_r);
 }
 
-template <bool TRACE>
-__global__ __launch_bounds__(BLOCK) void k_reset_tpe(Params p) {
-    __shared__ uint32_t lds[BLOCK * TPE_CW];
+// NB: threads per block.  Everything here is per wave (LDS image, copy-out), so small
+// batches launch 64-thread blocks: one wave per CU instead of four on a quarter of the CUs.
+template <bool TRACE, int NB = BLOCK>
+__global__ __launch_bounds__(NB) void k_reset_tpe(Params p) {
+    __shared__ uint32_t lds[NB * TPE_CW];
     const int lane = threadIdx.x & 63;
     uint32_t* img = lds + (threadIdx.x & ~63) * TPE_CW;
     uint32_t* me = img + lane * TPE_CW;
-    const int64_t env0 = (int64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63);
+    const int64_t env0 = (int64_t)blockIdx.x * NB + (threadIdx.x & ~63);
     const int64_t env = env0 + lane;
     const bool doit = env < p.B && (!p.reset_mask || p.reset_mask[env]);
     me[0] = 0;
@@ -275,13 +277,13 @@ __global__ __launch_bounds__(BLOCK) void k_reset_tpe(Params p) {
 
 // step() (:403-513) fused with next_request(), get_state(), reward, done and auto-reset.
 // RECOMPUTE (Philox mode, many envs): the scenario is redrawn instead of loaded.
-template <bool TRACE, bool RECOMPUTE>
-__global__ __launch_bounds__(BLOCK) void k_step_tpe(Params p) {
-    __shared__ uint32_t lds[BLOCK * TPE_CW];
+template <bool TRACE, bool RECOMPUTE, int NB = BLOCK>
+__global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
+    __shared__ uint32_t lds[NB * TPE_CW];
     const int lane = threadIdx.x & 63;
     uint32_t* img = lds + (threadIdx.x & ~63) * TPE_CW;
     uint32_t* me = img + lane * TPE_CW;
-    const int64_t env0 = (int64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63);
+    const int64_t env0 = (int64_t)blockIdx.x * NB + (threadIdx.x & ~63);
     const int64_t env = env0 + lane;
     const bool live = env < p.B;
     const int64_t ev = live ? env : 0;  // dead lanes read env 0 (harmless) and store nothing
