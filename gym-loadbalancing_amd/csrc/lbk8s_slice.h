@@ -499,7 +499,11 @@ __global__ __launch_bounds__(BLOCK) LB_SLICE_OCC void k_step_slice(Params p) {
 #pragma unroll
         for (int k = 0; k < EPL; ++k) {
             int e = lane + k * W;
+#ifdef LB_ABL_SLICE_ED_FULL
+            if (e < E) p.edyn[eidx(p, env, e)] = v.ed[k];  // whole row, coalesced
+#else
             if (e == ai || e == oA) p.edyn[eidx(p, env, e)] = v.ed[k];
+#endif
         }
     }
     if (p.obs && !(SPLIT && done && p.auto_reset)) slice_write_obs<W, EPL>(p, p.obs, env, lane, v);

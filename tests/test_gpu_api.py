@@ -88,22 +88,27 @@ def test_vecenv_sb3_surface():
     assert r.is_cuda and d.dtype == torch.bool
 
 
-def test_sharding_invariance_device():
+@pytest.mark.parametrize("sizes", [(2048, 2048), (65536, 100)])
+def test_sharding_invariance_device(sizes):
+    """Shards see their global env ids' trajectories.  (65536, 100): the whole batch runs
+    the 256-thread-block step kernel with a ragged tail, the shards the 64-thread one."""
     from lbk8s import LBVecEnv
-    B = 4096
+    B = sum(sizes)
+    offs = [sum(sizes[:i]) for i in range(len(sizes))]
     cfg = dict(num_endpoints=8, reward_function="fairness")
     full = LBVecEnv(B, seed=11, as_tensors=True, **cfg)
-    parts = [LBVecEnv(B // 2, seed=11, env_id_offset=o, as_tensors=True, **cfg) for o in (0, B // 2)]
+    parts = [LBVecEnv(n, seed=11, env_id_offset=o, as_tensors=True, **cfg) for n, o in zip(sizes, offs)]
     a0 = full.reset().clone()
     torch.testing.assert_close(a0, torch.cat([p.reset().clone() for p in parts]), rtol=0, atol=0)
     gen = torch.Generator(device="cuda")
     gen.manual_seed(0)
     for s in range(150):
         a = torch.randint(0, 9, (B,), dtype=torch.int32, device="cuda", generator=gen)
-        o1, r1, _, _ = full.step(a)
-        outs = [p.step(a[i * (B // 2):(i + 1) * (B // 2)]) for i, p in enumerate(parts)]
+        o1, r1, d1, _ = full.step(a)
+        outs = [p.step(a[o:o + n]) for n, o, p in zip(sizes, offs, parts)]
         assert torch.equal(o1, torch.cat([x[0] for x in outs]))
         assert torch.equal(r1, torch.cat([x[1] for x in outs]))
+        assert torch.equal(d1, torch.cat([x[2] for x in outs]))
 
 
 def test_full_size_properties():
