@@ -15,6 +15,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <cstring>
 #include <string>
@@ -246,7 +247,21 @@ constexpr bool kSplitReset = false;
 Geo geometry(const lb_config* c, int64_t B = 0) {
     Geo g;
     const int E = c->num_endpoints;
+    // E <= 8: one lane per env, except few envs (B < 32768, config 2), where lanes over
+    // endpoints (the wide slice shape) cut each wave's serial chain: 4096 default envs
+    // 10.8 -> 7.4 us per lb_step (tools/ablate.py, variant NO_SMALL_SLICE).
+    // LBK8S_GEOMETRY=tpe|slice pins the choice for E <= 8 (test hook; the state layout
+    // follows it, so it must not change during an env's life).
     g.tpe = E <= TPE_E;
+#ifndef LB_ABL_NO_SMALL_SLICE
+    if (g.tpe && B > 0 && B < WIDE_SLICE_MAX_B) g.tpe = false;
+#endif
+    if (E <= TPE_E) {
+        if (const char* f = getenv("LBK8S_GEOMETRY")) {
+            if (!strcmp(f, "tpe")) g.tpe = true;
+            else if (!strcmp(f, "slice")) g.tpe = false;
+        }
+    }
     if (g.tpe) {
         g.W = 1;
         g.EPL = 1;
@@ -278,7 +293,7 @@ struct Offsets {
 };
 
 Offsets offsets(const lb_config* c, int64_t B) {
-    Geo g = geometry(c);
+    Geo g = geometry(c, B);
     Offsets o;
     uint64_t x = 0;
     auto take = [&](uint64_t bytes) { uint64_t r = x; x = align_up(x + bytes); return r; };
@@ -338,7 +353,7 @@ int validate(const lb_config* c) {
 }
 
 Params make_params(void* state, const lb_config* c, int64_t B) {
-    Geo g = geometry(c);
+    Geo g = geometry(c, B);
     Offsets o = offsets(c, B);
     char* base = (char*)state;
     Params p;

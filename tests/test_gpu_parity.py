@@ -52,9 +52,20 @@ class GpuBackend:
         return {k: self.env.field(v).cpu().numpy() for k, v in FIELD_MAP.items()}
 
 
+def pin_geometry(monkeypatch, geometry, cfg):
+    """Below 32,768 envs E <= 8 runs the slice kernels; "tpe" pins the thread-per-env
+    kernels (liblbk8s reads LBK8S_GEOMETRY on every call) so both stay covered."""
+    if geometry == "tpe":
+        if cfg.get("num_endpoints", 8) > 8:
+            pytest.skip("thread-per-env kernels take E <= 8")
+        monkeypatch.setenv("LBK8S_GEOMETRY", "tpe")
+
+
+@pytest.mark.parametrize("geometry", ["auto", "tpe"])
 @pytest.mark.parametrize("name", golden_names())
-def test_kernel_trace_parity_with_reference(name):
+def test_kernel_trace_parity_with_reference(name, geometry, monkeypatch):
     d = load(os.path.join(GOLDEN, name + ".npz"))
+    pin_geometry(monkeypatch, geometry, dict(d["config"]))
     be = GpuBackend(d["config"], d["actions"].shape[0])
     policy = None
     if name.startswith("greedy_"):
@@ -76,11 +87,13 @@ PHILOX_CFGS = {
 }
 
 
+@pytest.mark.parametrize("geometry", ["auto", "tpe"])
 @pytest.mark.parametrize("name", sorted(PHILOX_CFGS))
-def test_philox_mode_matches_oracle(oracle_mod, name):
+def test_philox_mode_matches_oracle(oracle_mod, name, geometry, monkeypatch):
     """Same seed, same env ids, same actions -> identical trajectories (GPU vs C oracle)."""
     from lbk8s import LBVecEnv
     cfg = PHILOX_CFGS[name]
+    pin_geometry(monkeypatch, geometry, cfg)
     B = 2048 if cfg.get("num_endpoints", 8) <= 16 else 512
     seed, off = 12345, 7_000_000_000  # env ids above 2^32 exercise the counter's high word
     env = LBVecEnv(B, seed=seed, env_id_offset=off, **cfg)
