@@ -127,7 +127,10 @@ const char* lb_last_error(void);
 int lb_validate_config(const lb_config* cfg);
 
 /* Bytes of the opaque device state blob for num_envs envs (replaces the per-env
- * Python object state of LoadBalancerK8sEnv.__init__, :86-287). */
+ * Python object state of LoadBalancerK8sEnv.__init__, :86-287).  The blob's layout is a
+ * function of (cfg, num_envs): every call on one blob must pass the same num_envs, and
+ * the environment variable LBK8S_GEOMETRY (tpe|slice, a test hook for E <= 8) must not
+ * change during the blob's life. */
 int lb_state_bytes(const lb_config* cfg, int64_t num_envs, uint64_t* out_bytes);
 
 /* LoadBalancerK8sEnv.__init__ (:86-287) for all envs: lookup tables, zeroed
