@@ -2,18 +2,28 @@
 """Benchmark: vectorized LoadBalancerK8sEnv env-steps/s on MI355X (BASELINE.json config 3).
 
 One bench "step" = one vector step of every env on every GPU: the fused step kernel
-(lb_step: take_action + reward + next_request + get_state + auto-reset) consumes one
-batch of uniform-random actions (pre-generated on the device before timing: the random
-policy of BASELINE configs 2/3).  Observations, rewards and dones go into a T-deep device ring, the shape
-of PPO's rollout storage (ppo_deepset.py:136-143), so writes stream to HBM instead of
-sitting in the 256 MB Infinity Cache.  Inputs (env state) are resident in HBM.
+(lb_step: take_action + reward + next_request + get_state + auto-reset) with the env's
+uniform random policy drawn inside the kernel (lb_step with actions == NULL; the random
+policy of BASELINE configs 2/3, the same draws lb_policy(random) returns).  Observations,
+rewards and dones go into a T-deep device ring, the shape of PPO's rollout storage
+(ppo_deepset.py:136-143), so writes stream to HBM instead of sitting in the 256 MB
+Infinity Cache; terminal observations and episode-statistics rows of finished envs are
+written too.  Env state is resident in HBM before timing.
 
-Default workload: 2^20 default-scenario envs per GPU (E=8, N=24, Z=4, rejection, naive,
-episode_length 100; Philox seed 0).  Multi-GPU: one process per GPU, env ids sharded
-[rank*B, (rank+1)*B) with no data-path collective ("scaling": "weak").
+Episodes are staggered before timing (env i starts at step i mod episode_length), so every
+timed step ends and auto-resets 1/episode_length of the envs — the steady state of a
+long-running VecEnv — whatever --steps is; the count of resets inside the timed window is
+reported.
+
+Default workload: 2^20 default-scenario envs IN TOTAL (E=8, N=24, Z=4, rejection, naive,
+episode_length 100; Philox seed 0), sharded over the GPUs: rank r owns global env ids
+[r*B/G, (r+1)*B/G) with no data-path collective ("scaling": "strong").  --weak keeps
+--envs per GPU instead.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       torchrun --nproc-per-node N bench.py --gpus N ...
+  With --gpus N > 1 and no torchrun environment, bench.py launches N ranks itself
+  (torch.distributed.run, 127.0.0.1) before touching the GPU and exits with their status.
+  --plan-only: the launcher / sharding / statistics-reduction path without a GPU (gloo).
 """
 import argparse
 import json
@@ -28,6 +38,7 @@ for _p in (REPO, os.path.join(REPO, "gym-loadbalancing_amd")):
 
 METRIC = "env-steps/sec (whole node) at 1M envs, 1/2/4/8 GPUs; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+REFERENCE_SUBPROC_8CORE = 2858.0  # the reference itself, 8-worker pipe VecEnv, survey container
 
 CONFIGS = {
     "default": dict(),  # constructor defaults, loadbalancer_k8s_env.py:42-54
@@ -38,33 +49,40 @@ CONFIGS = {
 }
 
 
-def algorithmic_bytes(cfg):
-    """B_alg = 53*E + 6*Z + 240 (rejection) / + 208 (no rejection).
+def algorithmic_bytes(cfg, reads_actions=True):
+    """B_alg = 53*E + 6*Z + 240 (rejection) / + 208 (no rejection), which
+    counts a 4-byte action read; the on-device random policy reads no action.
 
     Z here is the observable zone block (zone ids are drawn in [0,4) whatever num_zones
     is, loadbalancer_k8s_env.py:354), i.e. the survey's Z=4 default.
     """
     E = cfg.num_endpoints
     Z = min(cfg.num_zones, 4) if cfg.num_zones >= 4 else cfg.num_zones
-    return 53 * E + 6 * Z + (240 if cfg.rejection_allowed else 208)
+    b = 53 * E + 6 * Z + (240 if cfg.rejection_allowed else 208)
+    return b if reads_actions else b - 4
 
 
-def parse():
+def parse(argv):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--envs-per-gpu", type=int, default=1 << 20)
+    ap.add_argument("--envs", type=int, default=1 << 20, help="envs in total (per GPU with --weak)")
+    ap.add_argument("--weak", action="store_true", help="--envs per GPU (weak scaling)")
     ap.add_argument("--config", default="default", choices=sorted(CONFIGS))
     ap.add_argument("--ring", type=int, default=16, help="rollout ring depth (obs slots)")
+    ap.add_argument("--no-graph", action="store_true", help="launch every step eagerly")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--plan-only", action="store_true", help="launcher + sharding + stats reduction, no GPU")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def cpu_baseline(cfg_kwargs, seconds):
-    """The C oracle (Philox mode, OpenMP over envs) on a bounded sample of the same workload."""
+    """The C oracle (Philox mode, OpenMP over envs) on a bounded sample of the same workload,
+    plus the reference's process pattern (SubprocVecEnv: one worker process per core, one
+    Pipe round trip per vector step) around the same oracle, one env per worker."""
     import numpy as np
 
     from oracle import oracle
@@ -84,81 +102,153 @@ def cpu_baseline(cfg_kwargs, seconds):
         if el >= seconds:
             break
     _ = np.zeros(1)
-    return dict(value=B * steps / el, unit="env-steps/s", cores=oracle.num_threads(), kind="port",
-                sample=f"C oracle (oracle/lbk8s_oracle.c, OpenMP), {B} envs x {steps} vector steps "
-                       f"({el:.1f} s), same scenario, Philox seed 0, random policy")
+    out = dict(value=B * steps / el, unit="env-steps/s", cores=oracle.num_threads(), kind="port",
+               sample=f"C oracle (oracle/lbk8s_oracle.c, OpenMP), {B} envs x {steps} vector steps "
+                      f"({el:.1f} s), same scenario, Philox seed 0, random policy")
+    try:
+        out["subproc_vecenv"] = oracle.subproc_vecenv_rate(cfg_kwargs, workers=min(16, os.cpu_count() or 1),
+                                                           seconds=min(5.0, seconds))
+    except Exception as e:  # noqa: BLE001  (context only; never fails the bench)
+        out["subproc_vecenv"] = {"error": repr(e)}
+    out["reference_itself"] = {"value": REFERENCE_SUBPROC_8CORE, "cores": 8,
+                               "sample": "the reference env under an 8-worker pipe VecEnv, survey container "
+                                         "(BASELINE.md; the reference does not travel to the GPU box)"}
+    return out
 
 
-def main():
-    args = parse()
+def plan_only(args, rank, world):
+    """CPU path of the launcher: shard table and one episode-statistics all_reduce (gloo)."""
+    import torch
+    import torch.distributed as dist
+
+    from lbk8s.dist import reduce_episode_stats, shard
+    if world > 1:
+        dist.init_process_group("gloo")
+    off, n = shard(args.envs * (world if args.weak else 1), rank, world)
+    # a fake ep_stats block: every env of this rank finished one episode of return = its global id
+    st = torch.zeros((n, 16), dtype=torch.float64)
+    st[:, 0] = torch.arange(off, off + n, dtype=torch.float64)
+    st[:, 1] = 100.0
+    red = reduce_episode_stats(st, torch.ones(n, dtype=torch.bool))
+    shards = [None] * world
+    if world > 1:
+        dist.all_gather_object(shards, (rank, off, n))
+    else:
+        shards = [(rank, off, n)]
+    if rank == 0:
+        print(json.dumps({"plan": True, "world": world, "shards": shards,
+                          "reduced": [float(x) for x in red]}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse(argv)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and world_env == 1:
+        # launch the ranks ourselves (before any GPU call), wait, and report their status
+        from lbk8s.dist import launch
+        raise SystemExit(launch(args.gpus, os.path.abspath(__file__), argv))
+    if world_env != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world = world_env
+    if args.plan_only:
+        return plan_only(args, rank, world)
+
     import torch
     import torch.distributed as dist
 
     from lbk8s import LBVecEnv
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from lbk8s.dist import shard
+    from lbk8s.info import ST_EPISODE
+    if torch.cuda.device_count() < world:
+        raise SystemExit(f"bench.py: {world} ranks but {torch.cuda.device_count()} visible GPUs")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    B = args.envs_per_gpu
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+    total = args.envs * (world if args.weak else 1)
+    off, B = shard(total, rank, world)
     cfg_kwargs = CONFIGS[args.config]
-    env = LBVecEnv(B, device=dev, seed=0, env_id_offset=rank * B, as_tensors=True, **cfg_kwargs)
+    env = LBVecEnv(B, device=dev, seed=0, env_id_offset=off, as_tensors=True, **cfg_kwargs)
     R = env.cfg.obs_rows
+    L = env.cfg.episode_length
     T = max(1, args.ring)
     obs_ring = torch.empty((T, B, R, 8), dtype=torch.float32, device=dev)
     rew_ring = torch.empty((T, B), dtype=torch.float32, device=dev)
     done_ring = torch.empty((T, B), dtype=torch.uint8, device=dev)
-    K = args.steps
-    # synthetic input resident in HBM before timing: uniform-random actions (the random
-    # policy of BASELINE config 2/3) for every step of both passes
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(1234 + rank)
-    actions = torch.randint(0, env.action_space.n, (args.warmup + 2 * K, B), dtype=torch.int32,
-                            device=dev, generator=gen)
+    stream = torch.cuda.current_stream(dev)
+
+    def one_step(i):  # actions=None: the env's random policy, drawn inside the step kernel
+        env.step_device(None, obs_out=obs_ring[i % T], reward_out=rew_ring[i % T], done_out=done_ring[i % T])
+
+    # setup: stagger the episodes so 1/L of the envs end (and auto-reset) at every step
     env.reset()
+    gid = torch.arange(off, off + B, device=dev)
+    for r in range(1, L):
+        one_step(0)
+        env.reset_masked((gid % L) == r)
+    # one graph of T steps (ring slots 0..T-1): no host launch cost between the kernels
+    graph = None
+    if not args.no_graph:
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(stream)
+        with torch.cuda.stream(side):
+            one_step(0)
+        stream.wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for i in range(T):
+                one_step(i)
 
-    def one_step(i, ev=None):
-        if ev is not None:
-            ev[0].record()
-        env.step_device(actions[i], obs_out=obs_ring[i % T], reward_out=rew_ring[i % T],
-                        done_out=done_ring[i % T])
-        if ev is not None:
-            ev[1].record()
+    def run(first, count):
+        i, end = first, first + count
+        while i < end:
+            if graph is not None and i % T == 0 and end - i >= T:
+                graph.replay()
+                i += T
+            else:
+                one_step(i)
+                i += 1
 
-    for i in range(args.warmup):
-        one_step(i)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
-    # pass 1: wall clock of exactly K steps, barrier + synchronize on both sides
+    run(0, args.warmup)
+    K = args.steps
+    ep0 = env.stats()[:, ST_EPISODE].sum().item()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # timed: exactly K steps, barrier + synchronize on both sides; HIP events on the step
+    # kernels' stream bracket the same K launches (their average = the kernel's duration)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(K):
-        one_step(args.warmup + i)
+    ev0.record(stream)
+    run(args.warmup, K)
+    ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    own_el = el
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    # pass 2: per-launch duration of the dominant kernel (lb_step) with events on its stream
-    torch.cuda.synchronize()
-    for i in range(K):
-        one_step(args.warmup + K + i, evs[i])
-    torch.cuda.synchronize()
-    step_ms = sum(a.elapsed_time(b) for a, b in evs) / K
+    kernel_ms = ev0.elapsed_time(ev1) / K
+    resets = int(env.stats()[:, ST_EPISODE].sum().item() - ep0)
     assert env.status() == 0, "kernel flagged bad actions / unreset envs"
+    assert kernel_ms <= own_el / K * 1e3 * 1.001, "event window longer than the wall-clock window"
+    if world > 1:
+        v = torch.tensor([float(resets), float(B)], dtype=torch.float64, device=dev)
+        dist.all_reduce(v)
+        resets = int(v[0].item())
 
-    value = world * B * K / el
-    b_alg = algorithmic_bytes(env.cfg)
-    achieved = b_alg * B / (step_ms * 1e-3) / 1e9
+    value = total * K / el
+    b_alg = algorithmic_bytes(env.cfg, reads_actions=False)
+    achieved = b_alg * B / (kernel_ms * 1e-3) / 1e9
     traffic = None
     try:
         with open(args.pmc_json) as f:
@@ -170,16 +260,18 @@ def main():
     line = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": K,
         "warmup": args.warmup, "ms_per_step": el / K * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic (Philox seed 0 scenarios; uniform-random actions pre-generated in HBM)",
-        "config": {"workload": f"config 3: {B} {args.config}-scenario envs per GPU "
-                               f"(E={env.cfg.num_endpoints}, N={env.cfg.num_nodes}, "
-                               f"Z={env.cfg.num_zones}, {env.cfg.reward_function}), obs ring T={T}",
-                   "envs_per_gpu": B, "total_envs": world * B, "scenario": args.config,
-                   "episode_length": env.cfg.episode_length, "parallelism": f"env-sharded x{world}"},
+        "scaling": "weak" if args.weak else "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (Philox seed 0 scenarios; the env's uniform random policy drawn on the device)",
+        "config": {"workload": f"config 3: {total} {args.config}-scenario envs in total "
+                               f"(E={env.cfg.num_endpoints}, N={env.cfg.num_nodes}, Z={env.cfg.num_zones}, "
+                               f"{env.cfg.reward_function}), {B} per GPU, obs ring T={T}, staggered episodes",
+                   "envs_per_gpu": B, "total_envs": total, "scenario": args.config, "episode_length": L,
+                   "resets_in_window": resets, "graphs": graph is not None,
+                   "parallelism": f"env-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_step (lb_step)", "kernel_ms": step_ms, "bytes_per_env_step": b_alg},
+                     "kernel": "k_step_tpe (lb_step)" if env.cfg.num_endpoints <= 8 else "k_step_slice (lb_step)",
+                     "kernel_ms": kernel_ms, "bytes_per_env_step": b_alg, "envs_per_launch": B},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(cfg_kwargs, args.cpu_seconds)

@@ -227,51 +227,31 @@ struct Geo {
 // E > 8: W-lane slices.  Few envs (B < 32768): one env per wave (W = 16/32/64 by E), so
 // the launch still has thousands of waves; many envs: 4 envs per wave up to E = 64, so
 // the per-env scalar chain (Philox, logs, reward) is issued once per 4 envs and 4x more
-// envs are in flight per CU.  Measured at E = 64 (tools/ablate.py): 2^20 envs 1.45 ->
+// envs are in flight per CU.  Measured at E = 64 (A/B builds, profiles/r01_ablation.jsonl): 2^20 envs 1.45 ->
 // 1.00 ms per step, 4096 envs 8.9 vs 20.7 us.  Both shapes give the same EP = W * EPL
 // (the next power of two >= max(E, 16)), so the state layout does not depend on B.
-[[maybe_unused]] constexpr int64_t WIDE_SLICE_MAX_B = 32768;
+constexpr int64_t WIDE_SLICE_MAX_B = 32768;
 // E <= 8, few envs (config 2: 4096): 64-thread blocks, so the batch spreads over 4x more
-// CUs (every TPE kernel works per wave).  LB_ABL_TPE_BLOCK256 keeps 256-thread blocks.
-#ifdef LB_ABL_TPE_BLOCK256
-constexpr int64_t SMALL_TPE_MAX_B = 0;
-#else
+// CUs (every TPE kernel works per wave).
 constexpr int64_t SMALL_TPE_MAX_B = 65536;
-#endif
-#if defined(LB_ABL_SPLIT_RESET) || defined(LB_ABL_SCEN_SPLIT)
-constexpr bool kSplitReset = true;
-#else
-constexpr bool kSplitReset = false;
-#endif
 
 Geo geometry(const lb_config* c, int64_t B = 0) {
     Geo g;
     const int E = c->num_endpoints;
     // E <= 8: one lane per env, except few envs (B < 32768, config 2), where lanes over
     // endpoints (the wide slice shape) cut each wave's serial chain: 4096 default envs
-    // 10.8 -> 7.4 us per lb_step (tools/ablate.py, variant NO_SMALL_SLICE).
-    // LBK8S_GEOMETRY=tpe|slice pins the choice for E <= 8 (test hook; the state layout
-    // follows it, so it must not change during an env's life).
+    // 10.8 -> 7.4 us per lb_step (A/B builds, profiles/r01_ablation.jsonl).
+    // cfg->geometry pins the choice for E <= 8 (the state layout follows it).
     g.tpe = E <= TPE_E;
-#ifndef LB_ABL_NO_SMALL_SLICE
     if (g.tpe && B > 0 && B < WIDE_SLICE_MAX_B) g.tpe = false;
-#endif
-    if (E <= TPE_E) {
-        if (const char* f = getenv("LBK8S_GEOMETRY")) {
-            if (!strcmp(f, "tpe")) g.tpe = true;
-            else if (!strcmp(f, "slice")) g.tpe = false;
-        }
-    }
+    if (E <= TPE_E && c->geometry == LB_GEOMETRY_TPE) g.tpe = true;
+    if (c->geometry == LB_GEOMETRY_SLICE) g.tpe = false;
     if (g.tpe) {
         g.W = 1;
         g.EPL = 1;
         g.EP = E;
     } else {
-#ifdef LB_ABL_WIDE_SLICE
-        const bool wide = true;
-#else
         const bool wide = B < WIDE_SLICE_MAX_B;
-#endif
         if (wide) {
             g.W = E <= 16 ? 16 : E <= 32 ? 32 : 64;
             g.EPL = E <= 64 ? 1 : E <= 128 ? 2 : 4;
@@ -348,6 +328,7 @@ int validate(const lb_config* c) {
     if (c->episode_length < 1 || c->episode_length > CMAX) return fail("episode_length must be in [1, 1023]");
     if (c->reward_fn < 0 || c->reward_fn > 3) return fail("unknown reward_fn");
     if (c->rng_mode != LB_RNG_PHILOX && c->rng_mode != LB_RNG_TRACE) return fail("unknown rng_mode");
+    if (c->geometry < LB_GEOMETRY_AUTO || c->geometry > LB_GEOMETRY_SLICE) return fail("unknown geometry");
     if (!(c->arrival_rate > 0.0)) return fail("arrival_rate must be > 0");
     return 0;
 }
@@ -530,7 +511,7 @@ int lb_step(void* state, const lb_config* cfg, int64_t num_envs, const int32_t* 
     Geo g = geometry(cfg, num_envs);
     hipStream_t s = (hipStream_t)stream;
     if (g.tpe) {
-        const bool recompute = kRecomputeScenario && num_envs >= SCEN_RECOMPUTE_MIN_B;
+        const bool recompute = num_envs >= SCEN_RECOMPUTE_MIN_B;
         if (num_envs <= SMALL_TPE_MAX_B && !recompute) {
             const unsigned nb = (unsigned)((num_envs + 63) / 64);
             if (tr) hipLaunchKernelGGL((k_step_tpe<true, false, 64>), dim3(nb), dim3(64), 0, s, p);
@@ -542,23 +523,10 @@ int lb_step(void* state, const lb_config* cfg, int64_t num_envs, const int32_t* 
         else hipLaunchKernelGGL((k_step_tpe<false, false>), dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);
         return check_launch();
     }
-    // many-env shape, kSplitReset: finished envs are reset by a second launch masked by
-    // the done flags
-    const bool split = kSplitReset && num_envs >= WIDE_SLICE_MAX_B && cfg->auto_reset && done_out;
     LB_DISPATCH_SLICE(g.W, g.EPL, {
         const unsigned nb = slice_blocks(num_envs, W);
-        if (split) {
-            Params q = p;
-            q.reset_mask = done_out;
-            if (tr) hipLaunchKernelGGL((k_step_slice<W, EPL, true, true>), dim3(nb), dim3(BLOCK), 0, s, p);
-            else hipLaunchKernelGGL((k_step_slice<W, EPL, false, true>), dim3(nb), dim3(BLOCK), 0, s, p);
-            if (int r = check_launch()) return r;
-            if (tr) hipLaunchKernelGGL((k_reset_slice<W, EPL, true>), dim3(nb), dim3(BLOCK), 0, s, q);
-            else hipLaunchKernelGGL((k_reset_slice<W, EPL, false>), dim3(nb), dim3(BLOCK), 0, s, q);
-        } else {
-            if (tr) hipLaunchKernelGGL((k_step_slice<W, EPL, true, false>), dim3(nb), dim3(BLOCK), 0, s, p);
-            else hipLaunchKernelGGL((k_step_slice<W, EPL, false, false>), dim3(nb), dim3(BLOCK), 0, s, p);
-        }
+        if (tr) hipLaunchKernelGGL((k_step_slice<W, EPL, true>), dim3(nb), dim3(BLOCK), 0, s, p);
+        else hipLaunchKernelGGL((k_step_slice<W, EPL, false>), dim3(nb), dim3(BLOCK), 0, s, p);
     });
     return check_launch();
 }

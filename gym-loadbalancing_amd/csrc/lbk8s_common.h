@@ -192,30 +192,10 @@ struct Params {
 
 // Streaming stores for the observation stream (written once per step, consumed later
 // by the learner): nontemporal, so they do not displace state lines from L2 / MALL.
-// Measured on MI355X at 2^20 default envs: step 0.191 -> 0.108 ms (tools/ablate.py).
+// Measured on MI355X at 2^20 default envs: step 0.191 -> 0.108 ms (A/B builds, profiles/r01_ablation.jsonl).
 typedef float f4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st_stream(float4* p, float4 v) {
-#ifdef LB_ABL_PLAIN_OBS
-    *p = v;
-#else
     __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(p));
-#endif
-}
-template <typename T>
-__device__ __forceinline__ void st_state(T* p, T v) {
-#ifdef LB_ABL_NT_STATE
-    __builtin_nontemporal_store(v, p);
-#else
-    *p = v;
-#endif
-}
-template <typename T>
-__device__ __forceinline__ T ld_state(const T* p) {
-#ifdef LB_ABL_NT_LOAD
-    return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
 }
 
 __device__ __forceinline__ int64_t eidx(const Params& p, int64_t env, int e) {

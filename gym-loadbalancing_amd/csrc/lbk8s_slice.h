@@ -11,16 +11,6 @@
 
 namespace lbk {
 
-#ifdef LB_ABL_SLICE_OCC4
-#define LB_SLICE_OCC __attribute__((amdgpu_waves_per_eu(4)))
-#else
-#define LB_SLICE_OCC
-#endif
-#if defined(LB_ABL_SLICE_SCEN) || defined(LB_ABL_SCEN_SPLIT)
-constexpr bool kSliceScenario = true;   // Philox mode: recompute lat0 / emeta / topology
-#else
-constexpr bool kSliceScenario = false;
-#endif
 
 template <int W>
 __device__ __forceinline__ int slice_sum(int v) {
@@ -96,35 +86,6 @@ struct SEnv {
 };
 
 // get_state() (:688-758): rows [zone, zone_cpu_cap, cpu, topo_lat, lat, req_zone, thr, dt]
-#ifdef LB_ABL_SLICE_ROWS
-// (ablation: each lane stores its own 32-byte rows as two 16-byte halves; a store
-// instruction then covers every other 16 bytes and the nontemporal halves reach HBM as
-// partial writes: 2,947 B written per env-step at E = 64 instead of ~2,190)
-template <int W, int EPL>
-__device__ __forceinline__ void slice_write_obs(const Params& p, float* out, int64_t env, int lane,
-                                                const SEnv<EPL>& v) {
-    float* base = out + env * (int64_t)p.R * 8;
-    const float rz = (float)v.s.rz, thr = (float)threshold(v.s.thr_idx), dt = (float)v.dt;
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) {
-        int e = lane + k * W;
-        if (e < p.E) {
-            int z = em_zone(v.em[k]);
-            float4 a = make_float4((float)z, (float)zcap_val(v.zcap, z), v.ocpu[k],
-                                   (float)topo_val(v.topo, z, v.s.rz));
-            float4 b = make_float4(v.olat[k], rz, thr, dt);
-            float4* row = reinterpret_cast<float4*>(base + e * 8);
-            st_stream(row, a);
-            st_stream(row + 1, b);
-        }
-    }
-    if (p.rejection && lane == (p.E % W)) {
-        float4* row = reinterpret_cast<float4*>(base + p.E * 8);
-        st_stream(row, make_float4(-1.f, -1.f, -1.f, -1.f));
-        st_stream(row + 1, make_float4(-1.f, rz, thr, dt));
-    }
-}
-#else
 // The env's R x 32-byte block is written as contiguous runs: store c covers float4s
 // cW .. cW + W - 1 of the block (rows cW/2 .. cW/2 + W/2 - 1), lane l the float4 2r + h of
 // row r = cW/2 + (l >> 1), h = l & 1.  Row r < E is endpoint r, held by lane r % W in
@@ -163,51 +124,14 @@ __device__ __forceinline__ void slice_write_obs(const Params& p, float* out, int
         }
     }
 }
-#endif
 
-// Philox mode: the lane's endpoints of the episode (reset() :328, :379-386) drawn again
-// instead of loaded (the draws are a pure function of seed, env id and episode)
 template <int W, int EPL>
-__device__ __forceinline__ void slice_scenario(const Params& p, int64_t env, int lane, uint32_t episode,
-                                               SEnv<EPL>& v) {
-    int node[EPL];
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) {
-        const int e = lane + k * W;
-        node[k] = 0;
-        v.lat0[k] = 0.0;
-        if (e < p.E) {
-            U4 w = draw(p, env, episode, (uint32_t)e, D_EP);
-            v.lat0[k] = 1.0 + 99.0 * u53(w.x, w.y);
-            node[k] = (int)bounded(w.z, 24);
-        }
-    }
-    int owner[EPL];  // first endpoint hosted on the same node (shares its cpu)
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) owner[k] = lane + k * W;
-    for (int e2 = 0; e2 < p.E; ++e2) {
-        const int nd2 = shfl_u32<W>((uint32_t)sel<EPL>(node, e2 / W), e2 % W);
-#pragma unroll
-        for (int k = 0; k < EPL; ++k) owner[k] = (nd2 == node[k] && e2 < owner[k]) ? e2 : owner[k];
-    }
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) {
-        const int e = lane + k * W;
-        int ty = 0, zo = 0, cpu = 0;
-        if (e < p.E) node_draw<false>(p, env, episode, node[k], ty, zo, cpu);
-        v.em[k] = e < p.E ? em_pack(zo, owner[k], ty, cpu, node[k]) : 0u;
-    }
-}
-
-template <int W, int EPL, bool STORED = true>
 __device__ __forceinline__ void slice_load(const Params& p, int64_t env, int lane, SEnv<EPL>& v) {
 #pragma unroll
     for (int k = 0; k < EPL; ++k) {
         int64_t i = eidx(p, env, lane + k * W);
-        if constexpr (STORED) {
-            v.lat0[k] = p.lat0[i];
-            v.em[k] = p.emeta[i];
-        }
+        v.lat0[k] = p.lat0[i];
+        v.em[k] = p.emeta[i];
         v.ed[k] = p.edyn[i];
     }
     v.t = p.t[env];
@@ -215,17 +139,9 @@ __device__ __forceinline__ void slice_load(const Params& p, int64_t env, int lan
     v.zcap = p.zcap[env];
     v.acc2 = p.acc2[env];
     v.acc3 = p.acc3[env];
-    if constexpr (STORED) {
-        v.topo = p.topo[env];
-        v.nz0 = p.nzone[env];
-        v.nz1 = p.NZW > 1 ? p.nzone[p.B + env] : 0;
-    } else {
-        const uint32_t episode = (uint32_t)(v.acc3 >> 32);
-        slice_scenario<W, EPL>(p, env, lane, episode, v);
-        v.topo = scen_topo(p, env, episode);
-        v.nz0 = 0;
-        v.nz1 = 0;
-    }
+    v.topo = p.topo[env];
+    v.nz0 = p.nzone[env];
+    v.nz1 = p.NZW > 1 ? p.nzone[p.B + env] : 0;
     v.sum_lat = p.sum_lat[env];
     v.sum_cpu = p.sum_cpu[env];
     v.total = p.total[env];
@@ -245,7 +161,7 @@ __device__ __forceinline__ void slice_store_scalars(const Params& p, int64_t env
 }
 
 // the request part of next_request() (:1131-1163); the dequeue part is folded into the LUTs
-template <int W, bool TRACE, int EPL, bool DRAW_ZONE = false>
+template <int W, bool TRACE, int EPL>
 __device__ __forceinline__ void slice_next_request(const Params& p, int64_t env, int lane, bool from_reset,
                                                    SEnv<EPL>& v) {
     double x1, x2;
@@ -257,14 +173,8 @@ __device__ __forceinline__ void slice_next_request(const Params& p, int64_t env,
     v.dt = departure - arrival;
     v.t = arrival;
     v.s.thr_idx = (r + 6) % 7;  // endpoint_list[r - 1] (:1117)
-    if constexpr (DRAW_ZONE) {  // the zone of the request's node (:1120-1121), drawn again
-        int ty, zo, cpu;
-        node_draw<false>(p, env, (uint32_t)(v.acc3 >> 32), n, ty, zo, cpu);
-        v.s.rz = zo;
-    } else {
-        uint64_t word = n < 32 ? v.nz0 : (n < 64 ? v.nz1 : p.nzone[(n >> 5) * p.B + env]);
-        v.s.rz = (int)((word >> (2 * (n & 31))) & 3);
-    }
+    const uint64_t word = n < 32 ? v.nz0 : (n < 64 ? v.nz1 : p.nzone[(n >> 5) * p.B + env]);
+    v.s.rz = (int)((word >> (2 * (n & 31))) & 3);
 }
 
 // reset() (:290-400) into registers, then the per-episode state stores.
@@ -382,18 +292,15 @@ __global__ __launch_bounds__(BLOCK) void k_reset_slice(Params p) {
 }
 
 // step() (:403-513) fused with next_request(), get_state(), reward, done and auto-reset.
-// SPLIT: the reset of envs that finish is left to a k_reset_slice launch masked by the
-// done flags, so reset()'s draws do not raise this kernel's register count.
-template <int W, int EPL, bool TRACE, bool SPLIT>
-__global__ __launch_bounds__(BLOCK) LB_SLICE_OCC void k_step_slice(Params p) {
-    constexpr bool stored = TRACE || !kSliceScenario;
+template <int W, int EPL, bool TRACE>
+__global__ __launch_bounds__(BLOCK) void k_step_slice(Params p) {
     const int lane = threadIdx.x % W;
     const int64_t env = (int64_t)blockIdx.x * (BLOCK / W) + threadIdx.x / W;
     if (env >= p.B) return;
     const int E = p.E;
     // ---- phase 0: independent loads (state + action)
     SEnv<EPL> v;
-    slice_load<W, EPL, stored>(p, env, lane, v);
+    slice_load<W, EPL>(p, env, lane, v);
     const int a = p.actions ? p.actions[env] : random_action(p, env, v.acc3, v.s.step);  // fused random policy
 
     // ---- phase 1: decode, then every table lookup the step needs, issued together
@@ -424,14 +331,8 @@ __global__ __launch_bounds__(BLOCK) LB_SLICE_OCC void k_step_slice(Params p) {
         // (j > 0) / refreshed (m > 0) gather from the LUTs
         const int j = ed_j(v.ed[k]), m = ed_m(v.ed[k]);
         double l = v.lat0[k], c = (double)em_c0(v.em[k]);
-#ifdef LB_ABL_ALWAYS_LUT
-        l = p.lat_lut[j * LAT_ROWS + (int)v.lat0[k]];
-        if (j == 0) l = v.lat0[k];
-        c = p.cpu_lut[m * CPU_ROWS + em_c0(v.em[k])];
-#else
         if (j) l = p.lat_lut[j * LAT_ROWS + (int)v.lat0[k]];
         if (m) c = p.cpu_lut[m * CPU_ROWS + em_c0(v.em[k])];
-#endif
         v.olat[k] = (float)l;
         v.ocpu[k] = (float)c;
     }
@@ -484,7 +385,7 @@ __global__ __launch_bounds__(BLOCK) LB_SLICE_OCC void k_step_slice(Params p) {
     v.total += reward;
 
     // ---- next_request (:1131-1163), done (:472), outputs
-    slice_next_request<W, TRACE, EPL, !stored>(p, env, lane, false, v);
+    slice_next_request<W, TRACE, EPL>(p, env, lane, false, v);
     const bool done = v.s.step == p.L;
     if (lane == 0) {
         if (p.reward) p.reward[env] = (float)reward;
@@ -494,19 +395,15 @@ __global__ __launch_bounds__(BLOCK) LB_SLICE_OCC void k_step_slice(Params p) {
         if (p.term_obs) slice_write_obs<W, EPL>(p, p.term_obs, env, lane, v);
         if (p.ep_stats && lane == 0)
             write_stats_row(p, p.ep_stats + env * LB_ST_K, v.s, v.acc2, v.acc3, v.total, v.sum_lat, v.sum_cpu);
-        if constexpr (!SPLIT) slice_reset<W, EPL, TRACE>(p, env, lane, v);
+        slice_reset<W, EPL, TRACE>(p, env, lane, v);
     } else if (accept) {
 #pragma unroll
         for (int k = 0; k < EPL; ++k) {
             int e = lane + k * W;
-#ifdef LB_ABL_SLICE_ED_FULL
-            if (e < E) p.edyn[eidx(p, env, e)] = v.ed[k];  // whole row, coalesced
-#else
             if (e == ai || e == oA) p.edyn[eidx(p, env, e)] = v.ed[k];
-#endif
         }
     }
-    if (p.obs && !(SPLIT && done && p.auto_reset)) slice_write_obs<W, EPL>(p, p.obs, env, lane, v);
+    if (p.obs) slice_write_obs<W, EPL>(p, p.obs, env, lane, v);
     if (lane == 0) slice_store_scalars<EPL>(p, env, v);
 }
 

@@ -39,10 +39,6 @@ __device__ __forceinline__ void tpe_request_draws(const Params& p, int64_t env, 
             x1 = p.tr.step_x1[env]; x2 = p.tr.step_x2[env]; r = p.tr.step_r[env]; n = p.tr.step_n[env];
         }
     } else {  // draw map: (D_REQ_X) -> x1 words 0,1 / x2 words 2,3; (D_REQ_I) -> r word 0 / n word 1
-#ifdef LB_ABL_NO_RNG
-        x1 = 0.01; x2 = 1.0; r = (int)(slot % 7); n = (int)(env % p.N);
-        return;
-#endif
         U4 a = draw(p, env, episode, slot, D_REQ_X);
         U4 b = draw(p, env, episode, slot, D_REQ_I);
         x1 = p.inv_rate * std_exp(a.x, a.y);
@@ -56,17 +52,12 @@ __device__ __forceinline__ void tpe_request_draws(const Params& p, int64_t env, 
 // cpu, topology) is a pure function of (seed, global env id, episode), so the step
 // recomputes what it needs instead of loading it: 19 Philox blocks replace 112 of the
 // ~220 bytes per env-step it reads (lat0 f64 + emeta per endpoint, topology, node zones).
-// Measured (tools/ablate.py, default scenario): 2^20 envs 0.111 -> 0.107 ms, 2^22 envs
+// Measured (A/B builds, profiles/r01_ablation.jsonl, default scenario): 2^20 envs 0.111 -> 0.107 ms, 2^22 envs
 // 0.678 -> 0.591 ms; but below 2^18 envs, where a step is latency bound rather than
 // bandwidth bound, the serial Philox work lengthens each wave (4096 envs 12.6 -> 15.0 us),
 // so lb_step recomputes only from SCEN_RECOMPUTE_MIN_B envs.  reset() still stores the
 // scenario (lb_get_field / lb_policy read it); trace mode keeps the stored scenario (its
 // values come from the reference's generator).
-#ifdef LB_ABL_STORED_SCEN
-constexpr bool kRecomputeScenario = false;
-#else
-constexpr bool kRecomputeScenario = true;
-#endif
 constexpr int64_t SCEN_RECOMPUTE_MIN_B = 1 << 18;
 
 // endpoint latencies / packed metadata of the episode (reset() :328, :379-386)
@@ -240,14 +231,14 @@ __device__ void tpe_reset(const Params& p, int64_t env, TEnv& v, uint32_t* me) {
 }
 
 __device__ __forceinline__ void tpe_store_scalars(const Params& p, int64_t env, const TEnv& v) {
-    st_state(p.t + env, v.t);
-    st_state(p.sc + env, sc_pack(v.s));
-    st_state(p.acc2 + env, v.acc2);
-    st_state(p.acc3 + env, v.acc3);
-    st_state(p.sum_lat + env, v.sum_lat);
-    st_state(p.sum_cpu + env, v.sum_cpu);
-    st_state(p.total + env, v.total);
-    if (p.reward_fn != LB_REWARD_NAIVE) st_state(p.last_r + env, v.last_r);
+    *(p.t + env) = (v.t);
+    *(p.sc + env) = (sc_pack(v.s));
+    *(p.acc2 + env) = (v.acc2);
+    *(p.acc3 + env) = (v.acc3);
+    *(p.sum_lat + env) = (v.sum_lat);
+    *(p.sum_cpu + env) = (v.sum_cpu);
+    *(p.total + env) = (v.total);
+    if (p.reward_fn != LB_REWARD_NAIVE) *(p.last_r + env) = (v.last_r);
 }
 
 // NB: threads per block.  Everything here is per wave (LDS image, copy-out), so small
@@ -298,22 +289,22 @@ __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
     for (int e = 0; e < TPE_E; ++e) {
         const int64_t i = (int64_t)e * p.B + ev;
         if constexpr (stored) {
-            lat0[e] = e < E ? ld_state(p.lat0 + i) : 0.0;
-            em[e] = e < E ? ld_state(p.emeta + i) : 0u;
+            lat0[e] = e < E ? *(p.lat0 + i) : 0.0;
+            em[e] = e < E ? *(p.emeta + i) : 0u;
         }
-        ed[e] = e < E ? ld_state(p.edyn + i) : 0u;
+        ed[e] = e < E ? *(p.edyn + i) : 0u;
     }
-    int a = p.actions ? ld_state(p.actions + ev) : 0;
-    v.t = ld_state(p.t + ev);
-    v.s = sc_unpack(ld_state(p.sc + ev));
-    v.zcap = ld_state(p.zcap + ev);
-    v.acc2 = ld_state(p.acc2 + ev);
-    v.acc3 = ld_state(p.acc3 + ev);
+    int a = p.actions ? *(p.actions + ev) : 0;
+    v.t = *(p.t + ev);
+    v.s = sc_unpack(*(p.sc + ev));
+    v.zcap = *(p.zcap + ev);
+    v.acc2 = *(p.acc2 + ev);
+    v.acc3 = *(p.acc3 + ev);
     if (!p.actions) a = random_action(p, ev, v.acc3, v.s.step);  // fused random policy
     if constexpr (stored) {
-        v.topo = ld_state(p.topo + ev);
-        v.nz0 = ld_state(p.nzone + ev);
-        v.nz1 = p.NZW > 1 ? ld_state(p.nzone + p.B + ev) : 0;
+        v.topo = *(p.topo + ev);
+        v.nz0 = *(p.nzone + ev);
+        v.nz1 = p.NZW > 1 ? *(p.nzone + p.B + ev) : 0;
     } else {
         const uint32_t episode = (uint32_t)(v.acc3 >> 32);
         tpe_scenario(p, ev, episode, lat0, em);
@@ -321,10 +312,10 @@ __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
         v.nz0 = 0;
         v.nz1 = 0;
     }
-    v.sum_lat = ld_state(p.sum_lat + ev);
-    v.sum_cpu = ld_state(p.sum_cpu + ev);
-    v.total = ld_state(p.total + ev);
-    v.last_r = p.reward_fn != LB_REWARD_NAIVE ? ld_state(p.last_r + ev) : 0.0;
+    v.sum_lat = *(p.sum_lat + ev);
+    v.sum_cpu = *(p.sum_cpu + ev);
+    v.total = *(p.total + ev);
+    v.last_r = p.reward_fn != LB_REWARD_NAIVE ? *(p.last_r + ev) : 0.0;
 
     // ---- phase 1: decode the action, pick the selected endpoint, table lookups
     v.s.step = v.s.step < 0xFFFF ? v.s.step + 1 : 0xFFFF;
@@ -356,21 +347,12 @@ __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
     for (int e = 0; e < TPE_E; ++e) {
         if (e < E) {
             const int j = ed_j(ed[e]);
-#ifdef LB_ABL_NO_LUT
-            const double l = lat0[e];
-            const double c = (double)em_c0(em[e]);
-#elif defined(LB_ABL_ALWAYS_LUT)
-            double l = p.lat_lut[(j) * LAT_ROWS + (int)lat0[e]];
-            if (j == 0) l = lat0[e];
-            const double c = p.cpu_lut[ed_m(ed[e]) * CPU_ROWS + em_c0(em[e])];
-#else
             // table rows 0 are the initial values: only endpoints selected (j > 0) /
             // refreshed (m > 0) this episode gather from the LUTs
             const int m = ed_m(ed[e]);
             double l = lat0[e], c = (double)em_c0(em[e]);
             if (j) l = p.lat_lut[j * LAT_ROWS + (int)lat0[e]];
             if (m) c = p.cpu_lut[m * CPU_ROWS + em_c0(em[e])];
-#endif
             float ol = (float)l;
             float oc = (float)c;
             if (accept && e == ai) { ol = (float)next_lat; oc = (float)next_cpu; }
@@ -400,20 +382,10 @@ __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
         // decrease in next_request() (:1137-1143) -> the history counters advance
         const uint32_t edA_new = ((oA == ai ? (uint32_t)Mn : (uint32_t)ed_M(edA)) << 20) |
                                  ((uint32_t)Mn << 10) | (uint32_t)jn;
-#ifdef LB_ABL_ED_FULL
-        const uint32_t edO_new = (edO & ~(0x3FFu << 20)) | ((uint32_t)Mn << 20);
-#pragma unroll
-        for (int e = 0; e < TPE_E; ++e)
-            if (e == oA) ed[e] = edO_new;
-#pragma unroll
-        for (int e = 0; e < TPE_E; ++e)
-            if (e == ai) ed[e] = edA_new;
-#else
         if (live) {
-            if (oA != ai) st_state(p.edyn + (int64_t)oA * p.B + env, (edO & ~(0x3FFu << 20)) | ((uint32_t)Mn << 20));
-            st_state(p.edyn + (int64_t)ai * p.B + env, edA_new);
+            if (oA != ai) *(p.edyn + (int64_t)oA * p.B + env) = ((edO & ~(0x3FFu << 20)) | ((uint32_t)Mn << 20));
+            *(p.edyn + (int64_t)ai * p.B + env) = (edA_new);
         }
-#endif
         v.s.penalty = 0;
         reward = accept_reward(p, sel_lat, tl, sel_cpu, v.acc2, v.s.acc);
         v.last_r = reward;
@@ -447,7 +419,7 @@ __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
     }
     const bool done = live && v.s.step == p.L;  // (:472)
     if (live) {
-        if (p.reward) st_state(p.reward + env, (float)reward);
+        if (p.reward) *(p.reward + env) = ((float)reward);
         if (p.done) p.done[env] = (uint8_t)done;
     }
     tpe_image_env(me, v, done ? TPE_FLAG : 0);
@@ -465,17 +437,8 @@ __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
         }
     }
     if (live) tpe_store_scalars(p, env, v);
-#ifdef LB_ABL_ED_FULL
-    if (live && !do_reset) {
-#pragma unroll
-        for (int e = 0; e < TPE_E; ++e)
-            if (e < E) st_state(p.edyn + (int64_t)e * p.B + env, ed[e]);
-    }
-#endif
     __syncthreads();
-#ifndef LB_ABL_NO_OBS
     if (p.obs) tpe_copy_out(p, p.obs, img, env0, false);
-#endif
 }
 
 }  // namespace lbk

@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblbk8s.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 LB_REWARD = {"naive": 0, "latency": 1, "fairness": 2, "multi": 3}
 LB_RNG_PHILOX, LB_RNG_TRACE = 0, 1
@@ -22,6 +22,7 @@ LB_FIELD = {"endpoint_latency": 0, "endpoint_cpu_usage_percentage": 1,
 PER_ENV_FIELDS = {"current_time", "current_step", "request_zone", "request_threshold"}
 LB_ST_K = 16
 LB_STATUS_BAD_ACTION, LB_STATUS_NOT_RESET = 1, 2
+LB_GEOMETRY = {"auto": 0, "tpe": 1, "slice": 2}
 
 
 class LBConfigC(C.Structure):
@@ -30,7 +31,8 @@ class LBConfigC(C.Structure):
                 ("rejection_allowed", C.c_int32), ("auto_reset", C.c_int32), ("rng_mode", C.c_int32),
                 ("arrival_rate", C.c_double), ("call_duration", C.c_double),
                 ("latency_weight", C.c_double), ("cpu_weight", C.c_double),
-                ("gini_weight", C.c_double), ("seed", C.c_uint64), ("env_id_offset", C.c_int64)]
+                ("gini_weight", C.c_double), ("seed", C.c_uint64), ("env_id_offset", C.c_int64),
+                ("geometry", C.c_int32), ("reserved0", C.c_int32)]
 
 
 TRACE_FIELDS = ["t0", "step_x1", "step_x2", "step_r", "step_n", "reset_lat0", "reset_topo",

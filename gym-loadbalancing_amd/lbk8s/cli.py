@@ -13,11 +13,18 @@ Same flags and defaults as /root/reference/run.py:23-45, the same env constructi
     include (LBVecEnv can serve them as a VecEnv);
   * --testing runs the greedy evaluation of lbk8s.evaluate on the saved / given
     checkpoint (the reference's test_model, :130-161, plots one episode's reward);
-  * loading returns the agent (the reference's get_load_model returns load()'s None).
+  * loading returns the agent (the reference's get_load_model returns load()'s None);
+  * the training envs write VecMonitor's file, vec_loadbalancer_k8s_gym_results.monitor.csv
+    (run.py:122; one file per rank, suffixed, with --nproc > 1);
+  * --nproc N trains on N GPUs of the node: N ranks (one process per GPU, launched here
+    through torch.distributed.run), each with --num_envs envs of its own global env-id
+    range, gradients and episode statistics all-reduced over RCCL; rank 0 saves.
 """
 import argparse
 import json
 import logging
+import os
+import sys
 
 SB3_ALGS = ("ppo", "recurrent_ppo", "a2c", "mask_ppo")
 
@@ -53,6 +60,9 @@ def build_parser():
     p.add_argument("--test_episodes", default=1, type=int, help="episodes played side by side by --testing")
     p.add_argument("--device", default="cuda")
     p.add_argument("--seed", default=0, type=int, help="Philox seed of the envs")
+    p.add_argument("--nproc", default=1, type=int, help="GPUs (ranks) to train on, one process each")
+    p.add_argument("--monitor_file", default="vec_loadbalancer_k8s_gym_results",
+                   help="VecMonitor file of the training envs (run.py:122); '' disables it")
     return p
 
 
@@ -64,12 +74,13 @@ def env_kwargs(rejection, num_endpoints, num_zones, num_nodes, reward_function):
 
 
 def get_env(env_name, rejection, num_endpoints, num_zones, num_nodes, reward_function, num_envs=8,
-            device="cuda", seed=0):
+            device="cuda", seed=0, env_id_offset=0, monitor_file=None):
     if env_name != "loadbalancer":
         raise SystemExit("Invalid environment!")
     from .info import INFO_KEYS
     from .vec_env import LBVecEnv
-    return LBVecEnv(num_envs, device=device, seed=seed, as_tensors=True, monitor=True, info_keywords=INFO_KEYS,
+    return LBVecEnv(num_envs, device=device, seed=seed, env_id_offset=env_id_offset, as_tensors=True, monitor=True,
+                    info_keywords=INFO_KEYS, monitor_file=monitor_file or None,
                     **env_kwargs(rejection, num_endpoints, num_zones, num_nodes, reward_function))
 
 
@@ -94,7 +105,12 @@ def model_name(alg, env_name, num_endpoints, num_zones, reward, total_steps):
 
 
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     args = build_parser().parse_args(argv)
+    if args.nproc > 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        # spawn the ranks before anything touches the GPU, then wait for them
+        from .dist import launch
+        raise SystemExit(launch(args.nproc, "lbk8s.cli", argv, module=True))
     logging.info(args)
     alg, reward = args.alg, args.reward
     num_nodes, num_zones, num_endpoints = int(args.num_nodes), int(args.num_zones), int(args.num_endpoints)
@@ -102,14 +118,26 @@ def main(argv=None):
     name = model_name(alg, args.env_name, num_endpoints, num_zones, reward, total_steps)
     result = {"name": name}
     if args.training and not args.no_training:
+        from .dist import init_from_env
+        rank, world, dev = init_from_env("cuda" if str(args.device).startswith("cuda") else "cpu")
+        mon = args.monitor_file + (f"_rank{rank}" if world > 1 and args.monitor_file else "")
         env = get_env(args.env_name, args.rejection, num_endpoints, num_zones, num_nodes, reward,
-                      num_envs=args.num_envs, device=args.device, seed=args.seed)
+                      num_envs=args.num_envs, device=dev if world > 1 else args.device, seed=args.seed,
+                      env_id_offset=rank * args.num_envs, monitor_file=mon)
         model = get_model(alg, env)
         if args.loading:  # resume training
             model.load(args.load_path)
         model.learn(total_timesteps=total_steps)
-        model.save(name)
-        result["saved"] = name
+        env.close()
+        result.update(world_size=world, episode_returns=[float(r) for r in model.episode_returns[-3:]])
+        if rank == 0:
+            model.save(name)
+            result["saved"] = name
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+            if rank != 0:
+                return result
     if args.testing:
         from .evaluate import load_agent, run_test
         agent = load_agent(args.test_path, "ppo" if alg == "ppo_deepsets" else "dqn", device=args.device)

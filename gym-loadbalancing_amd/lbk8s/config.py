@@ -58,14 +58,14 @@ class LBConfig:
     def action_space(self):
         return Discrete(self.num_actions)
 
-    def to_c(self, seed=0, env_id_offset=0, auto_reset=True, trace=False):
+    def to_c(self, seed=0, env_id_offset=0, auto_reset=True, trace=False, geometry="auto"):
         return _native.LBConfigC(
             self.num_endpoints, self.num_zones, self.num_nodes, self.episode_length,
             _native.LB_REWARD[self.reward_function], int(bool(self.rejection_allowed)),
             int(bool(auto_reset)), _native.LB_RNG_TRACE if trace else _native.LB_RNG_PHILOX,
             float(self.arrival_rate_r), float(self.call_duration_r), float(self.latency_weight),
             float(self.cpu_weight), float(self.gini_weight), int(seed) & (2**64 - 1),
-            int(env_id_offset))
+            int(env_id_offset), _native.LB_GEOMETRY[geometry], 0)
 
     def as_dict(self):
         return asdict(self)

@@ -10,7 +10,8 @@ target_network_frequency steps (tau = 1, :199-203).  total_timesteps counts VECT
 (:122).
 
 Multi-GPU: gradients averaged with one all_reduce per train step (RCCL); every rank keeps
-its own envs and replay.
+its own envs and replay; the logged episode return is the mean over every rank's finished
+episodes (one 2-double all_reduce per log line).
 """
 import random
 import time
@@ -22,6 +23,7 @@ import torch.nn.functional as F
 from torch import optim
 
 from . import _native, fused
+from . import dist as lbdist
 from .deepsets import DQNDeepSetAgent, HUGE_NEG, allreduce_gradients
 
 
@@ -129,6 +131,8 @@ class DQN_DeepSets:
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed)
         self.q_network = DQNDeepSetAgent(env).to(self.device)
+        if lbdist.is_multi():
+            lbdist.broadcast_parameters(self.q_network)  # replicas start from rank 0's weights
         self.target_network = deepcopy(self.q_network)
         self.optimizer = optim.Adam(self.q_network.parameters(), lr=learning_rate)
         self.rb = DeviceReplayBuffer(buffer_size, self.num_envs, env.observation_space.shape, self.device, self.gen)
@@ -248,6 +252,7 @@ class DQN_DeepSets:
                 graphs[explore, self._parity].replay()
             else:
                 self._vector_step(obs, masks, explore, self._parity)
+            env.record_episodes(self._done_u8, self._rew, self._act)  # VecMonitor file, if any
             self._parity ^= 1
             self.rb.advance_host()
             if global_step > self.learning_starts and global_step % self.train_frequency == 0:
@@ -260,9 +265,10 @@ class DQN_DeepSets:
         return self
 
     def _flush_returns(self):
-        n = float(self._ep_cnt.sum().item())
-        if n > 0:
-            self.episode_returns.append(float(self._ep_sum.sum().item()) / n)
+        self.env.flush_monitor()
+        mean, _ = lbdist.mean_episode_return(self._ep_sum, self._ep_cnt)  # over every rank
+        if mean is not None:
+            self.episode_returns.append(mean)
         self._ep_sum.zero_()
         self._ep_cnt.zero_()
 

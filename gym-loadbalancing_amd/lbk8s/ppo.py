@@ -9,13 +9,17 @@ Reference quirk kept: actions are sampled WITHOUT masks during the rollout (:169
 masks are all True anyway, :808-821) and the stored masks are used in the update.
 
 Multi-GPU: one process per GPU, each with its own envs (LBVecEnv env_id_offset); the
-gradients are averaged with one all_reduce per optimizer step (RCCL over xGMI).
+gradients are averaged with one all_reduce per optimizer step (RCCL over xGMI) and the
+logged episode return is the mean over every rank's finished episodes.
 
-On one GPU the minibatch step (loss, fused forward/backward, clip_grad_norm, Adam) is
-captured once as a HIP graph and replayed per minibatch: ~200 launches per minibatch
-otherwise leave the GPU waiting on the host between the fused kernels.  The capture's
-warm-up steps are undone (parameters restored, Adam state zeroed), so the graph path
-computes the same update as the eager one.
+The minibatch step (loss, fused forward/backward, clip_grad_norm, Adam) is captured once
+as HIP graphs and replayed per minibatch: ~200 launches per minibatch otherwise leave the
+GPU waiting on the host between the fused kernels.  With several ranks the step is two
+graphs — loss/backward ending in the gradients packed into one flat bucket, then
+unpack/average + clip + Adam — with the bucket's all_reduce issued between them on the
+same stream (the collective stays outside the captures, so any backend works).  The
+capture's warm-up steps are undone (parameters restored, Adam state zeroed), so the graph
+path computes the same update as the eager one.
 """
 import time
 from typing import Optional
@@ -23,8 +27,9 @@ from typing import Optional
 import torch
 from torch import nn, optim
 
+from . import dist as lbdist
 from . import fused
-from .deepsets import DeepSetAgent, allreduce_gradients
+from .deepsets import DeepSetAgent
 
 
 def ppo_loss(agent, obs, actions, logprobs_old, masks, advantages, returns, values_old,
@@ -111,10 +116,14 @@ class PPO_DeepSets:
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed)
         self.agent = DeepSetAgent(env).to(self.device)
+        self._multi = lbdist.is_multi()
+        if self._multi:
+            lbdist.broadcast_parameters(self.agent)  # replicas start from rank 0's weights
+        # flat gradient bucket of the all_reduce (one collective per optimizer step)
+        self._gflat = torch.zeros(sum(p.numel() for p in self.agent.parameters()), device=self.device) \
+            if self._multi else None
         if use_graphs is None:
-            import torch.distributed as dist
-            multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
-            use_graphs = self.device.type == "cuda" and not multi
+            use_graphs = self.device.type == "cuda"
         # a captured step needs equal minibatches and a device-side Adam step / lr
         self.use_graphs = bool(use_graphs) and self.batch_size % self.minibatch_size == 0
         if self.use_graphs:
@@ -122,7 +131,7 @@ class PPO_DeepSets:
             self.optimizer = optim.Adam(self.agent.parameters(), lr=self._lr, eps=1e-5, capturable=True)
         else:
             self.optimizer = optim.Adam(self.agent.parameters(), lr=learning_rate, eps=1e-5)
-        self._mb_graph = None
+        self._mb_graphs = None
         T, B = num_steps, self.num_envs
         R, A = env.observation_space.shape[0], env.action_space.n
         dev = self.device
@@ -157,30 +166,55 @@ class PPO_DeepSets:
             # the env writes the next observation straight into the next storage slot
             next_obs = self.obs[step + 1] if step + 1 < T else self._last_obs
             env.step_device(self._act, obs_out=next_obs, reward_out=self.rewards[step], done_out=self._done_u8)
+            env.record_episodes(self._done_u8, self.rewards[step], self._act)  # VecMonitor file, if any
             next_done = self._done_u8.float()
             # finished-episode returns accumulate on the device (no per-step host sync)
             self._ep_sum += (env.ep_stats[:, 0] * next_done).sum()
             self._ep_cnt += next_done.sum()
-        n = float(self._ep_cnt.item())
-        if n > 0:
-            self.episode_returns.append(float(self._ep_sum.item()) / n)
+        env.flush_monitor()
+        mean, _ = lbdist.mean_episode_return(self._ep_sum, self._ep_cnt)  # over every rank
+        if mean is not None:
+            self.episode_returns.append(mean)
         self._ep_sum.zero_()
         self._ep_cnt.zero_()
         return next_obs, next_done
 
-    def _minibatch_step(self, obs, actions, logprobs, masks, adv, ret, val):
-        loss, pg, vl, ent, kl, cf = ppo_loss(
-            self.agent, obs, actions, logprobs, masks, adv, ret, val,
-            self.clip_coef, self.ent_coef, self.vf_coef, self.norm_adv, self.clip_vloss)
+    def _mb_backward(self, obs, actions, logprobs, masks, adv, ret, val):
+        """Loss and gradients of one minibatch; with several ranks the gradients end packed
+        in the flat bucket that the all_reduce averages."""
+        out = ppo_loss(self.agent, obs, actions, logprobs, masks, adv, ret, val,
+                       self.clip_coef, self.ent_coef, self.vf_coef, self.norm_adv, self.clip_vloss)
         self.optimizer.zero_grad(set_to_none=not self.use_graphs)
-        loss.backward()
-        allreduce_gradients(self.agent)
+        out[0].backward()
+        if self._multi:
+            torch.cat([p.grad.reshape(-1) for p in self.agent.parameters()], out=self._gflat)
+        return out
+
+    def _mb_apply(self):
+        """Averaged gradients (several ranks) -> clip_grad_norm -> Adam."""
+        if self._multi:
+            self._gflat /= torch.distributed.get_world_size()
+            off = 0
+            for p in self.agent.parameters():
+                n = p.numel()
+                p.grad.copy_(self._gflat[off:off + n].view_as(p))
+                off += n
         nn.utils.clip_grad_norm_(self.agent.parameters(), self.max_grad_norm)
         self.optimizer.step()
-        return loss, pg, vl, ent, kl, cf
+
+    def _allreduce(self):
+        if self._multi:
+            lbdist.all_reduce_sum(self._gflat)
+
+    def _minibatch_step(self, *mb):
+        out = self._mb_backward(*mb)
+        self._allreduce()
+        self._mb_apply()
+        return out
 
     def _capture(self, src, mb):
-        """Capture one minibatch step on static buffers (filled from minibatch `mb`)."""
+        """Capture one minibatch step on static buffers (filled from minibatch `mb`): one
+        graph on one rank, two graphs around the gradient all_reduce on several."""
         self._static = [torch.empty((self.minibatch_size,) + t.shape[1:], dtype=t.dtype, device=t.device)
                         for t in src]
         for d, t in zip(self._static, src):
@@ -193,9 +227,18 @@ class PPO_DeepSets:
             for _ in range(2):  # warm-up: allocates grads, Adam state, workspaces
                 self._minibatch_step(*self._static)
         torch.cuda.current_stream(self.device).wait_stream(side)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._static_out = self._minibatch_step(*self._static)
+        if self._multi:
+            ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(ga):
+                self._static_out = self._mb_backward(*self._static)
+            with torch.cuda.graph(gb):
+                self._mb_apply()
+            graphs = (ga, gb)
+        else:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._static_out = self._minibatch_step(*self._static)
+            graphs = (g,)
         with torch.no_grad():  # undo the warm-up steps
             for p, q in zip(params, snap):
                 p.copy_(q)
@@ -203,7 +246,15 @@ class PPO_DeepSets:
                 for v in st.values():
                     if isinstance(v, torch.Tensor):
                         v.zero_()
-        self._mb_graph = g
+        self._mb_graphs = graphs
+
+    def _replay(self):
+        if len(self._mb_graphs) == 1:
+            self._mb_graphs[0].replay()
+            return
+        self._mb_graphs[0].replay()
+        self._allreduce()  # eager collective on the current stream, between the two graphs
+        self._mb_graphs[1].replay()
 
     def update(self, next_obs, next_done):
         with torch.no_grad():
@@ -223,11 +274,11 @@ class PPO_DeepSets:
             for start in range(0, self.batch_size, self.minibatch_size):
                 mb = b_inds[start:start + self.minibatch_size]
                 if self.use_graphs:
-                    if self._mb_graph is None:
+                    if self._mb_graphs is None:
                         self._capture(src, mb)
                     for d, t in zip(self._static, src):
                         torch.index_select(t, 0, mb, out=d)
-                    self._mb_graph.replay()
+                    self._replay()
                     out = self._static_out
                 else:
                     out = self._minibatch_step(*(t[mb] for t in src))

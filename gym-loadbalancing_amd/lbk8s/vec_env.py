@@ -11,8 +11,12 @@ run.py:95-127 for the callers envs/ppo_deepset.py:145-189 and envs/dqn_deepset.p
 Semantics (SB3 VecEnv, documented there, not pinned by the reference's tests):
 auto-reset on done; infos[i]["terminal_observation"] holds the pre-reset obs; with
 monitor=True infos[i]["episode"] = {"r", "l", "t"} plus the info_keywords copied from
-the final info, like VecMonitor.  `infos` is lazy: a dict is built only when indexed
-(per-env Python dicts for 10^6 envs would cost more than the step itself).
+the final info, like VecMonitor, and with monitor_file=name every finished episode is
+appended to name.monitor.csv in VecMonitor's layout (run.py:122 wraps the training envs
+in VecMonitor(env, "vec_loadbalancer_k8s_gym_results", info_keywords)).  `infos` is
+lazy: a dict is built only when indexed (per-env Python dicts for 10^6 envs would cost
+more than the step itself).  seed(s) is applied at the next reset() (SB3's convention;
+the reference's own env.seed raises TypeError, loadbalancer_k8s_env.py:128,569).
 
 Every buffer is a torch tensor on the HIP device; calls are asynchronous on torch's
 current stream.  With as_tensors=True the step returns those device tensors (zero
@@ -20,6 +24,7 @@ copy); otherwise numpy copies (the reference callers wrap them in torch.Tensor()
 """
 import ctypes as C
 import csv
+import json
 import os
 import time
 
@@ -90,12 +95,39 @@ class LazyInfos:
         return info
 
 
+class _MonitorWriter:
+    """VecMonitor's results file (SB3 ResultsWriter): a '#' JSON header line, then one row
+    per finished episode: r, l, t (seconds since t_start) and the info keywords."""
+
+    def __init__(self, filename, t_start, info_keywords):
+        if not filename.endswith("monitor.csv"):
+            filename = os.path.join(filename, "monitor.csv") if os.path.isdir(filename) else filename + ".monitor.csv"
+        self.path = filename
+        self.t_start = t_start
+        self.keys = tuple(info_keywords)
+        self.f = open(filename, "w", newline="")
+        self.f.write("#" + json.dumps({"t_start": t_start, "env_id": "None"}) + "\n")
+        self.w = csv.writer(self.f)
+        self.w.writerow(["r", "l", "t"] + list(self.keys))
+        self.f.flush()
+
+    def write(self, rows, rewards, actions, t):
+        for st, r, a in zip(rows, rewards, actions):
+            info = step_info(st, float(r), int(a))
+            self.w.writerow([round(float(st[ST_RETURN]), 6), int(st[ST_LENGTH]), round(t - self.t_start, 6)]
+                            + [info[k] for k in self.keys])
+        self.f.flush()
+
+    def close(self):
+        self.f.close()
+
+
 class LBVecEnv:
     """B vectorized LoadBalancerK8sEnv instances resident on one HIP device."""
 
     def __init__(self, num_envs, device=None, seed=0, env_id_offset=0, trace=False, t0=None,
                  auto_reset=True, as_tensors=False, monitor=False, info_keywords=(),
-                 save_csv=False, **env_kwargs):
+                 save_csv=False, monitor_file=None, geometry="auto", **env_kwargs):
         import torch
         self.torch = torch
         self.cfg = LBConfig(**env_kwargs)
@@ -108,13 +140,15 @@ class LBVecEnv:
         self.trace_mode = bool(trace)
         self.auto_reset = bool(auto_reset)
         self.as_tensors = bool(as_tensors)
-        self.monitor = bool(monitor)
+        self.monitor = bool(monitor) or monitor_file is not None
         self.info_keywords = tuple(info_keywords)
+        self.geometry = geometry
         self.save_csv = bool(save_csv)
         self.env_id_offset = int(env_id_offset)
         self.observation_space = self.cfg.observation_space()
         self.action_space = self.cfg.action_space()
-        self._c = self.cfg.to_c(seed, env_id_offset, auto_reset, trace)
+        self._c = self.cfg.to_c(seed, env_id_offset, auto_reset, trace, geometry)
+        self._pending_seed = None
         self._L = _native.lib()
         nbytes = C.c_uint64()
         _native.check(self._L.lb_state_bytes(C.byref(self._c), self.num_envs, C.byref(nbytes)))
@@ -135,6 +169,8 @@ class LBVecEnv:
         self._episode_count = 0
         self._t_start = time.time()
         self._host_cache = {}
+        self._monitor = _MonitorWriter(monitor_file, self._t_start, self.info_keywords) if monitor_file else None
+        self._mon_pending = []
         if self.trace_mode:
             if t0 is None:
                 raise ValueError("trace mode needs t0 (current_time after __init__) per env")
@@ -196,6 +232,9 @@ class LBVecEnv:
     # ---- VecEnv API -----------------------------------------------------------------------------
     def reset(self, trace=None):
         """reset() of every env (loadbalancer_k8s_env.py:290-400) -> obs (B, R, 8) float32."""
+        if self._pending_seed is not None:  # seed() takes effect here, for every env at once
+            self._c.seed = self._pending_seed
+            self._pending_seed = None
         if self.trace_mode:
             if trace is None:
                 raise ValueError("trace mode: reset() needs the reset draws")
@@ -247,6 +286,9 @@ class LBVecEnv:
         infos = LazyInfos(self, self.rewards, self.actions, self.dones, self._t_start)
         if self.save_csv:
             self._write_csv()
+        if self._monitor is not None:
+            self.record_episodes()
+            self.flush_monitor()
         if self.as_tensors:
             return self.obs, self.rewards, dones_b, infos
         obs = self.obs.cpu().numpy()
@@ -301,12 +343,47 @@ class LBVecEnv:
         return indices
 
     def seed(self, seed=None):
-        """Re-key the Philox stream; takes effect at the next reset of each env."""
-        self._c.seed = int(seed or 0) & (2**64 - 1)
+        """Re-key the Philox stream at the next reset() (SB3 VecEnv convention).
+
+        Until then every env keeps its current key, auto-resets included: an episode never
+        mixes two keys (the step may redraw the current episode's scenario from the key)."""
+        self._pending_seed = int(seed or 0) & (2**64 - 1)
         return [seed] * self.num_envs
 
     def close(self):
+        if self._monitor is not None:
+            self.flush_monitor()
+            self._monitor.close()
         self.state = None
+
+    # ---- VecMonitor file ------------------------------------------------------------------------
+    def record_episodes(self, dones=None, rewards=None, actions=None):
+        """Queue the episodes finished by the last step for the monitor file (device copies;
+        the host reads them at flush_monitor).  The device learners call this after every
+        step_device with the buffers they passed it; the drop-in step() does it itself."""
+        if self._monitor is None:
+            return
+        d = self.dones if dones is None else dones
+        r = self.rewards if rewards is None else rewards
+        a = self.actions if actions is None else actions
+        self._mon_pending.append((d.clone(), self.ep_stats[:, :12].clone(), r.clone(), a.clone(), time.time()))
+        if len(self._mon_pending) >= 64:
+            self.flush_monitor()
+
+    def flush_monitor(self):
+        if self._monitor is None or not self._mon_pending:
+            return
+        for d, st, r, a, t in self._mon_pending:
+            dn = d.cpu().numpy().astype(bool)
+            if dn.any():
+                self._monitor.write(st.cpu().numpy()[dn], r.cpu().numpy()[dn], a.cpu().numpy()[dn], t)
+        self._mon_pending = []
+
+    def reset_masked(self, mask):
+        """reset() of the envs where mask (B,) is nonzero; the others keep their episode."""
+        m = mask.to(device=self.device, dtype=self.torch.uint8).contiguous()
+        _native.check(self._L.lb_reset(self._ptr(self.state), C.byref(self._c), self.num_envs, self._ptr(m),
+                                       self._ptr(self.obs), None, self._stream()))
 
     # ---- framework extras (device-resident) -----------------------------------------------------
     def step_device(self, actions, obs_out=None, terminal_obs_out=None, reward_out=None,

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LBK8S_ABI_VERSION 2
+#define LBK8S_ABI_VERSION 3
 
 /* reward_function names of loadbalancer_k8s_env.py:20-31 */
 enum { LB_REWARD_NAIVE = 0, LB_REWARD_LATENCY = 1, LB_REWARD_FAIRNESS = 2, LB_REWARD_MULTI = 3 };
@@ -74,6 +74,10 @@ enum {
     LB_ST_EPISODE = 11,     /* episode index of this env (1-based)           */
     LB_ST_K = 16
 };
+/* lb_config.geometry: which kernel shape (and so which state layout) serves E <= 8.
+ * AUTO picks by batch size (lanes over endpoints below 32,768 envs, one lane per env above);
+ * TPE / SLICE pin it (parity tests cover both).  E > 8 always uses the slice kernels. */
+enum { LB_GEOMETRY_AUTO = 0, LB_GEOMETRY_TPE = 1, LB_GEOMETRY_SLICE = 2 };
 /* lb_status flag bits */
 enum { LB_STATUS_BAD_ACTION = 1, LB_STATUS_NOT_RESET = 2 };
 
@@ -91,6 +95,8 @@ typedef struct lb_config {
     double latency_weight, cpu_weight, gini_weight;
     uint64_t seed;             /* Philox key                                  */
     int64_t env_id_offset;     /* global id of this shard's env 0             */
+    int32_t geometry;          /* LB_GEOMETRY_*; part of the state layout     */
+    int32_t reserved0;         /* must be 0                                   */
 } lb_config;
 
 /*
@@ -128,9 +134,8 @@ int lb_validate_config(const lb_config* cfg);
 
 /* Bytes of the opaque device state blob for num_envs envs (replaces the per-env
  * Python object state of LoadBalancerK8sEnv.__init__, :86-287).  The blob's layout is a
- * function of (cfg, num_envs): every call on one blob must pass the same num_envs, and
- * the environment variable LBK8S_GEOMETRY (tpe|slice, a test hook for E <= 8) must not
- * change during the blob's life. */
+ * function of (cfg, num_envs): every call on one blob must pass the same num_envs and
+ * cfg.geometry. */
 int lb_state_bytes(const lb_config* cfg, int64_t num_envs, uint64_t* out_bytes);
 
 /* LoadBalancerK8sEnv.__init__ (:86-287) for all envs: lookup tables, zeroed

@@ -528,3 +528,6 @@ void orc_philox(const uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t out[4]
     philox4x32_10(c, k0, k1, out);
 }
 double orc_log(double x) { return fd_log(x); }
+
+/* Re-key the Philox stream (LBVecEnv.seed(): applied at the next full reset). */
+void orc_set_seed(void* h, uint64_t seed) { ((orc_env*)h)->c.seed = seed; }

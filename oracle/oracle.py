@@ -6,6 +6,7 @@ The product package (gym-loadbalancing_amd/lbk8s) never does.
 import ctypes as C
 import os
 import subprocess
+import time
 
 import numpy as np
 
@@ -65,6 +66,7 @@ def lib():
         L.orc_philox.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
         L.orc_log.restype = C.c_double
         L.orc_log.argtypes = [C.c_double]
+        L.orc_set_seed.argtypes = [C.c_void_p, C.c_uint64]
         _lib = L
     return _lib
 
@@ -164,6 +166,63 @@ class OracleBatch:
         out = np.zeros(self.B, np.int32)
         lib().orc_policy_random(self.h, _p(out))
         return out
+
+    def set_seed(self, seed):
+        lib().orc_set_seed(self.h, int(seed) & (2**64 - 1))
+
+
+def _subproc_worker(conn, cfg, wid):
+    """One SubprocVecEnv-style worker: a single oracle env, one Pipe round trip per step."""
+    os.environ["OMP_NUM_THREADS"] = "1"
+    orc = OracleBatch(cfg, 1, trace=False, seed=0, env_id_offset=wid)
+    orc.init()
+    conn.send(orc.reset())
+    while True:
+        a = conn.recv()
+        if a is None:
+            break
+        obs, rew, done, _, _ = orc.step(np.asarray([a], np.int32))
+        conn.send((obs, rew, done))
+    conn.close()
+
+
+def subproc_vecenv_rate(cfg, workers, seconds=5.0):
+    """env-steps/s of the reference's process pattern (run.py:114-122: SubprocVecEnv, one
+    env per worker process, actions out and (obs, reward, done) back over a Pipe every
+    vector step), with the oracle's single env in each worker instead of the Python env."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    pipes, procs = [], []
+    for w in range(workers):
+        a, b = ctx.Pipe()
+        p = ctx.Process(target=_subproc_worker, args=(b, dict(cfg), w), daemon=True)
+        p.start()
+        pipes.append(a)
+        procs.append(p)
+    try:
+        for c in pipes:
+            c.recv()
+        A = int(cfg.get("num_endpoints", 8)) + (1 if cfg.get("rejection_allowed", True) else 0)
+        rng = np.random.default_rng(0)
+        steps = 0
+        t0 = time.perf_counter()
+        while True:
+            acts = rng.integers(0, A, size=workers)
+            for c, a in zip(pipes, acts):
+                c.send(int(a))
+            _ = np.stack([c.recv()[0] for c in pipes])
+            steps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+    finally:
+        for c in pipes:
+            c.send(None)
+        for p in procs:
+            p.join(timeout=10)
+    return dict(value=workers * steps / el, unit="env-steps/s", workers=workers, kind="port",
+                sample=f"SubprocVecEnv pattern: {workers} worker processes x 1 oracle env, Pipe per "
+                       f"vector step, {steps} vector steps ({el:.1f} s)")
 
 
 def philox(ctr, key):

@@ -172,3 +172,93 @@ def test_fused_random_policy_step(B, kw):
             assert torch.equal(getattr(envs[0], f), getattr(envs[1], f)), f
     assert torch.equal(envs[0].stats(), envs[1].stats())
     assert envs[1].status() == 0
+
+
+@pytest.mark.parametrize("B", [2048, 1 << 18])
+def test_seed_applies_at_next_reset(oracle_mod, B):
+    """seed() mid-episode changes nothing until the next reset(); from there every env runs
+    on the new key (the oracle re-keyed at the same point).  B = 2^18 takes the step that
+    redraws the episode's scenario from the key."""
+    from lbk8s import LBVecEnv
+    L = 8
+    env = LBVecEnv(B, seed=5, as_tensors=True, episode_length=L)
+    orc = oracle_mod.OracleBatch(dict(episode_length=L), B, trace=False, seed=5)
+    orc.init()
+    assert torch.equal(env.reset().cpu(), torch.from_numpy(orc.reset()))
+
+    def steps(n):
+        for _ in range(n):
+            a = orc.policy_random()
+            o1, r1, d1, _ = env.step(torch.from_numpy(a).cuda())
+            o2, r2, d2, _, _ = orc.step(a)
+            np.testing.assert_array_equal(o1.cpu().numpy(), o2)
+            np.testing.assert_array_equal(r1.cpu().numpy(), r2)
+            np.testing.assert_array_equal(d1.cpu().numpy(), d2)
+
+    steps(3)
+    env.seed(987654321)          # mid-episode: pending
+    steps(L + 2)                 # an auto-reset in between still uses the old key
+    orc.set_seed(987654321)
+    np.testing.assert_array_equal(env.reset().cpu().numpy(), orc.reset())
+    steps(L + 2)
+    assert env.status() == 0
+
+
+def test_masked_reset_matches_oracle(oracle_mod):
+    """reset_masked (the bench's episode staggering) == the oracle's masked reset."""
+    from lbk8s import LBVecEnv
+    B, L = 4096, 10
+    env = LBVecEnv(B, seed=3, as_tensors=True, episode_length=L)
+    orc = oracle_mod.OracleBatch(dict(episode_length=L), B, trace=False, seed=3)
+    orc.init()
+    env.reset()
+    orc.reset()
+    gid = np.arange(B)
+    for r in range(1, L):
+        a = orc.policy_random()
+        env.step(torch.from_numpy(a).cuda())
+        orc.step(a)
+        mask = (gid % L) == r
+        env.reset_masked(torch.from_numpy(mask).cuda())
+        o2 = orc.reset(mask=mask)
+        np.testing.assert_array_equal(env.obs.cpu().numpy()[mask], o2[mask])
+    steps = env.field("current_step").cpu().numpy()
+    np.testing.assert_array_equal(steps, (L - 1 - gid % L) % L)
+    for k in range(3):  # every step ends the episodes of one residue class
+        a = orc.policy_random()
+        o1, r1, d1, _ = env.step(torch.from_numpy(a).cuda())
+        o2, r2, d2, _, _ = orc.step(a)
+        np.testing.assert_array_equal(o1.cpu().numpy(), o2)
+        np.testing.assert_array_equal(d1.cpu().numpy(), (gid % L) == k)
+
+
+def test_vecmonitor_file_during_training(tmp_path):
+    """LBVecEnv(monitor_file=...) writes VecMonitor's CSV (run.py:122) from the drop-in
+    step and from a device learner's step_device loop."""
+    import csv as _csv
+    import json as _json
+
+    from lbk8s import INFO_KEYS, LBVecEnv
+    from lbk8s.ppo import PPO_DeepSets
+    f = str(tmp_path / "vec_loadbalancer_k8s_gym_results")
+    env = LBVecEnv(32, seed=1, monitor_file=f, info_keywords=INFO_KEYS, episode_length=5, reward_function="multi")
+    env.reset()
+    for s in range(10):
+        env.step(np.full(32, s % 9, np.int32))
+    env.close()
+    lines = open(f + ".monitor.csv").read().splitlines()
+    assert lines[0].startswith("#") and "t_start" in _json.loads(lines[0][1:])
+    rows = list(_csv.DictReader(lines[1:]))
+    assert len(rows) == 64 and list(rows[0])[:3] == ["r", "l", "t"]
+    assert all(int(r["l"]) == 5 for r in rows)
+    assert set(INFO_KEYS) <= set(rows[0])
+    g = str(tmp_path / "ppo_run")
+    env = LBVecEnv(64, seed=2, as_tensors=True, monitor_file=g, info_keywords=INFO_KEYS, episode_length=10,
+                   reward_function="multi", latency_weight=1.0, cpu_weight=0.0, gini_weight=0.0)
+    algo = PPO_DeepSets(env, num_steps=20, n_minibatches=2, update_epochs=1, seed=2)
+    algo.learn(total_timesteps=64 * 20 * 2)
+    env.close()
+    rows = list(_csv.DictReader(open(g + ".monitor.csv").read().splitlines()[1:]))
+    assert len(rows) == 64 * 4  # 2 updates x 20 steps / episode length 10
+    rets = np.array([float(r["r"]) for r in rows])
+    assert abs(rets.mean() - np.mean(algo.episode_returns)) < 1e-3 * max(1.0, abs(rets.mean()))

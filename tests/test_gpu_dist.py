@@ -1,0 +1,54 @@
+"""Multi-rank learners on the GPU: 2 ranks, launched like the driver's
+bench (torch.distributed.run on 127.0.0.1).  On a one-GPU box both ranks share the card
+over gloo (LBK8S_DIST_BACKEND=gloo); the code path is the RCCL one minus the backend."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+
+def _env():
+    env = dict(os.environ, LBK8S_DIST_BACKEND="gloo", PYTHONPATH=os.path.join(REPO, "gym-loadbalancing_amd"))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    return env
+
+
+def test_ppo_two_ranks_graph_equals_eager(tmp_path):
+    """Averaged gradients keep the replicas identical, and the split-graph minibatch step
+    (graphs around the gradient all_reduce) computes the eager update."""
+    from lbk8s.dist import free_port
+    out = tmp_path / "res.json"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(REPO, "tests", "dist_ppo_worker.py"), str(out)]
+    r = subprocess.run(cmd, env=_env(), capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(out.read_text())
+    assert res["world"] == 2
+    assert res["ranks_agree_graphs0"] and res["ranks_agree_graphs1"], res
+    assert res["graph_eq_eager"], res
+    assert res["returns_eq"], res
+
+
+def test_cli_nproc_two_ranks(tmp_path):
+    """python -m lbk8s.cli --nproc 2: two ranks train, rank 0 saves, each rank writes its
+    VecMonitor file."""
+    r = subprocess.run([sys.executable, "-m", "lbk8s.cli", "--alg", "ppo_deepsets", "--nproc", "2",
+                        "--num_envs", "32", "--total_steps", str(32 * 100 * 2), "--num_endpoints", "8",
+                        "--rejection"], cwd=tmp_path, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert any(ln.get("world_size") == 2 and "saved" in ln for ln in lines), r.stdout[-2000:]
+    for rank in (0, 1):
+        mon = tmp_path / f"vec_loadbalancer_k8s_gym_results_rank{rank}.monitor.csv"
+        assert mon.exists()
+        assert len(mon.read_text().splitlines()) == 2 + 32 * 2  # header lines + 2 episodes per env
+    saved = [p for p in os.listdir(tmp_path) if p.startswith("ppo_deepsets_env_loadbalancer")]
+    assert len(saved) == 1

@@ -29,13 +29,13 @@ FIELD_MAP = dict(ep_lat="endpoint_latency", ep_cpu="endpoint_cpu_usage_percentag
 
 
 class GpuBackend:
-    def __init__(self, cfg, B):
-        self.cfg, self.B = cfg, B
+    def __init__(self, cfg, B, geometry="auto"):
+        self.cfg, self.B, self.geometry = cfg, B, geometry
         self.env = None
 
     def init(self, t0):
         from lbk8s import LBVecEnv
-        self.env = LBVecEnv(self.B, trace=True, t0=t0, **self.cfg)
+        self.env = LBVecEnv(self.B, trace=True, t0=t0, geometry=self.geometry, **self.cfg)
 
     def reset(self, ra):
         return self.env.reset(trace=ra)
@@ -52,21 +52,19 @@ class GpuBackend:
         return {k: self.env.field(v).cpu().numpy() for k, v in FIELD_MAP.items()}
 
 
-def pin_geometry(monkeypatch, geometry, cfg):
+def pin_geometry(geometry, cfg):
     """Below 32,768 envs E <= 8 runs the slice kernels; "tpe" pins the thread-per-env
-    kernels (liblbk8s reads LBK8S_GEOMETRY on every call) so both stay covered."""
-    if geometry == "tpe":
-        if cfg.get("num_endpoints", 8) > 8:
-            pytest.skip("thread-per-env kernels take E <= 8")
-        monkeypatch.setenv("LBK8S_GEOMETRY", "tpe")
+    kernels (lb_config.geometry) so both stay covered."""
+    if geometry == "tpe" and cfg.get("num_endpoints", 8) > 8:
+        pytest.skip("thread-per-env kernels take E <= 8")
 
 
 @pytest.mark.parametrize("geometry", ["auto", "tpe"])
 @pytest.mark.parametrize("name", golden_names())
-def test_kernel_trace_parity_with_reference(name, geometry, monkeypatch):
+def test_kernel_trace_parity_with_reference(name, geometry):
     d = load(os.path.join(GOLDEN, name + ".npz"))
-    pin_geometry(monkeypatch, geometry, dict(d["config"]))
-    be = GpuBackend(d["config"], d["actions"].shape[0])
+    pin_geometry(geometry, dict(d["config"]))
+    be = GpuBackend(d["config"], d["actions"].shape[0], geometry)
     policy = None
     if name.startswith("greedy_"):
         kind = name[len("greedy_"):].replace("_e64", "")
@@ -89,14 +87,14 @@ PHILOX_CFGS = {
 
 @pytest.mark.parametrize("geometry", ["auto", "tpe"])
 @pytest.mark.parametrize("name", sorted(PHILOX_CFGS))
-def test_philox_mode_matches_oracle(oracle_mod, name, geometry, monkeypatch):
+def test_philox_mode_matches_oracle(oracle_mod, name, geometry):
     """Same seed, same env ids, same actions -> identical trajectories (GPU vs C oracle)."""
     from lbk8s import LBVecEnv
     cfg = PHILOX_CFGS[name]
-    pin_geometry(monkeypatch, geometry, cfg)
+    pin_geometry(geometry, cfg)
     B = 2048 if cfg.get("num_endpoints", 8) <= 16 else 512
     seed, off = 12345, 7_000_000_000  # env ids above 2^32 exercise the counter's high word
-    env = LBVecEnv(B, seed=seed, env_id_offset=off, **cfg)
+    env = LBVecEnv(B, seed=seed, env_id_offset=off, geometry=geometry, **cfg)
     orc = oracle_mod.OracleBatch(cfg, B, trace=False, seed=seed, env_id_offset=off)
     orc.init()
     np.testing.assert_array_equal(env.reset(), orc.reset())

@@ -200,3 +200,55 @@ def test_gloo_world2_gradient_allreduce():
     mean = (expect[0] + expect[1]) / 2
     np.testing.assert_allclose(out[0], mean, rtol=1e-6, atol=1e-7)
     np.testing.assert_array_equal(out[0], out[1])
+
+
+def test_bench_launcher_creates_ranks():
+    """bench.py --gpus 2 (no torchrun environment) launches 2 ranks itself; --plan-only runs
+    the sharding + episode-statistics reduction path on gloo without a GPU."""
+    import json
+    import subprocess
+    import sys
+    from conftest import REPO
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--plan-only",
+                          "--envs", "1000001"], capture_output=True, text=True, env=env, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["world"] == 2
+    shards = sorted(tuple(x) for x in line["shards"])
+    assert [r for r, _, _ in shards] == [0, 1]
+    assert shards[0][1:] == (0, 500001) and shards[1][1:] == (500001, 500000)
+    n = 1000001
+    # every env "finished" with return = its global id: the reduction sees all of them
+    assert line["reduced"] == [float(n), float(n * (n - 1) // 2), 100.0 * n, 0.0]
+    # a world size that disagrees with --gpus is an error, never a silent 1-GPU run
+    env2 = dict(env, WORLD_SIZE="1")
+    bad = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "3", "--plan-only"],
+                         capture_output=True, text=True, env=dict(env2, WORLD_SIZE="2"), timeout=120)
+    assert bad.returncode != 0 and "WORLD_SIZE" in (bad.stdout + bad.stderr)
+
+
+def _mean_return_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from lbk8s.dist import mean_episode_return
+    s = torch.tensor([10.0 * (rank + 1)], dtype=torch.float64)
+    n = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    q.put((rank, mean_episode_return(s, n)))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_mean_episode_return():
+    """The learners' logged return is the mean over every rank's finished episodes."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mean_return_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0] == res[1] == ((10.0 + 20.0) / 3.0, 3.0)

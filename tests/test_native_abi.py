@@ -38,9 +38,50 @@ def test_library_exports_every_declared_symbol():
 
 def test_struct_sizes_match_header_layout():
     from lbk8s import _native
-    # 8 x int32 + 5 x double + uint64 + int64 = 32 + 40 + 16
-    assert C.sizeof(_native.LBConfigC) == 88
+    # 8 x int32 + 5 x double + uint64 + int64 + 2 x int32 = 32 + 40 + 16 + 8
+    assert C.sizeof(_native.LBConfigC) == 96
     assert C.sizeof(_native.LBTraceC) == 15 * 8
+
+
+def test_struct_offsets_match_compiled_header(tmp_path):
+    """Every ctypes field offset equals offsetof() of the C compiler on include/lbk8s.h."""
+    import subprocess
+
+    from lbk8s import _native
+    structs = {"lb_config": _native.LBConfigC, "lb_trace": _native.LBTraceC, "lb_ds_weights": _native.LBDSWeightsC}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "lbk8s.h"', "int main(void) {"]
+    for cname, cls in structs.items():
+        lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
+        for f, _ in cls._fields_:
+            lines.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "off.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "off"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {tuple(l.split()[:2]): int(l.split()[2]) for l in out if l}
+    for cname, cls in structs.items():
+        assert got[(cname, "sizeof")] == C.sizeof(cls), cname
+        for f, _ in cls._fields_:
+            assert got[(cname, f)] == getattr(cls, f).offset, (cname, f)
+
+
+def test_geometry_is_a_config_field():
+    """The E <= 8 kernel shape (and so the state layout) is chosen by lb_config.geometry."""
+    from lbk8s import LBConfig, _native
+    L = _native.lib()
+    sizes = {}
+    for g in ("auto", "tpe", "slice"):
+        c = LBConfig().to_c(geometry=g)
+        n = C.c_uint64()
+        assert L.lb_state_bytes(C.byref(c), 4096, C.byref(n)) == 0
+        sizes[g] = n.value
+    assert sizes["auto"] == sizes["slice"] != sizes["tpe"]  # 4096 envs: lanes over endpoints
+    c = LBConfig().to_c()
+    c.geometry = 7
+    assert L.lb_validate_config(C.byref(c)) != 0
+    assert b"geometry" in L.lb_last_error()
 
 
 def test_validate_and_state_bytes_host_only():
