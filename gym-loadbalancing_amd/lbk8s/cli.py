@@ -110,7 +110,9 @@ def main(argv=None):
     if args.nproc > 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
         # spawn the ranks before anything touches the GPU, then wait for them
         from .dist import launch
-        raise SystemExit(launch(args.nproc, "lbk8s.cli", argv, module=True))
+        child = [a for i, a in enumerate(argv)  # the ranks get the torchrun environment instead
+                 if not a.startswith("--nproc") and not (i > 0 and argv[i - 1] == "--nproc")]
+        raise SystemExit(launch(args.nproc, "lbk8s.cli", child, module=True))
     logging.info(args)
     alg, reward = args.alg, args.reward
     num_nodes, num_zones, num_endpoints = int(args.num_nodes), int(args.num_zones), int(args.num_endpoints)
