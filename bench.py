@@ -72,6 +72,7 @@ def parse(argv):
     ap.add_argument("--config", default="default", choices=sorted(CONFIGS))
     ap.add_argument("--ring", type=int, default=16, help="rollout ring depth (obs slots)")
     ap.add_argument("--no-graph", action="store_true", help="launch every step eagerly")
+    ap.add_argument("--lockstep", action="store_true", help="do not stagger episodes (all envs reset together)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--plan-only", action="store_true", help="launcher + sharding + stats reduction, no GPU")
@@ -189,7 +190,7 @@ def main(argv=None):
     # setup: stagger the episodes so 1/L of the envs end (and auto-reset) at every step
     env.reset()
     gid = torch.arange(off, off + B, device=dev)
-    for r in range(1, L):
+    for r in range(1, 1 if args.lockstep else L):
         one_step(0)
         env.reset_masked((gid % L) == r)
     # one graph of T steps (ring slots 0..T-1): no host launch cost between the kernels
@@ -264,7 +265,8 @@ def main(argv=None):
         "data": "synthetic (Philox seed 0 scenarios; the env's uniform random policy drawn on the device)",
         "config": {"workload": f"config 3: {total} {args.config}-scenario envs in total "
                                f"(E={env.cfg.num_endpoints}, N={env.cfg.num_nodes}, Z={env.cfg.num_zones}, "
-                               f"{env.cfg.reward_function}), {B} per GPU, obs ring T={T}, staggered episodes",
+                               f"{env.cfg.reward_function}), {B} per GPU, obs ring T={T}, "
+                               + ("lockstep" if args.lockstep else "staggered") + " episodes",
                    "envs_per_gpu": B, "total_envs": total, "scenario": args.config, "episode_length": L,
                    "resets_in_window": resets, "graphs": graph is not None,
                    "parallelism": f"env-sharded x{world}"},

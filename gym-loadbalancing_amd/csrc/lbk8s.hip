@@ -269,7 +269,7 @@ uint64_t align_up(uint64_t x) { return (x + 255) & ~(uint64_t)255; }
 
 struct Offsets {
     uint64_t lat_lut, cpu_lut, lat0, emeta, edyn, t, sc, topo, zcap, nzone, acc2, acc3, sum_lat,
-        sum_cpu, total, last_r, end;
+        sum_cpu, total, last_r, rs_cnt, rs_ids, end;
 };
 
 Offsets offsets(const lb_config* c, int64_t B) {
@@ -294,6 +294,10 @@ Offsets offsets(const lb_config* c, int64_t B) {
     o.sum_cpu = take(B * 8);
     o.total = take(B * 8);
     o.last_r = take(B * 8);
+    // deferred auto-reset lists of the thread-per-env step (k_step_tpe -> k_reset_listed)
+    const uint64_t nseg = g.tpe ? ((uint64_t)B + 63) / 64 : 0;
+    o.rs_cnt = take(nseg * 4);
+    o.rs_ids = take(nseg * 64 * 4);
     o.end = x;
     return o;
 }
@@ -355,6 +359,8 @@ Params make_params(void* state, const lb_config* c, int64_t B) {
     p.sum_cpu = (double*)(base + o.sum_cpu);
     p.total = (double*)(base + o.total);
     p.last_r = (double*)(base + o.last_r);
+    p.rs_cnt = (uint32_t*)(base + o.rs_cnt);
+    p.rs_ids = (uint32_t*)(base + o.rs_ids);
     p.B = B;
     p.env_id_offset = c->env_id_offset;
     p.es = g.tpe ? B : 1;
@@ -516,11 +522,19 @@ int lb_step(void* state, const lb_config* cfg, int64_t num_envs, const int32_t* 
             const unsigned nb = (unsigned)((num_envs + 63) / 64);
             if (tr) hipLaunchKernelGGL((k_step_tpe<true, false, 64>), dim3(nb), dim3(64), 0, s, p);
             else hipLaunchKernelGGL((k_step_tpe<false, false, 64>), dim3(nb), dim3(64), 0, s, p);
-            return check_launch();
+        } else if (tr) {
+            hipLaunchKernelGGL((k_step_tpe<true, false>), dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);
+        } else if (recompute) {
+            hipLaunchKernelGGL((k_step_tpe<false, true>), dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);
+        } else {
+            hipLaunchKernelGGL((k_step_tpe<false, false>), dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);
         }
-        if (tr) hipLaunchKernelGGL((k_step_tpe<true, false>), dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);
-        else if (recompute) hipLaunchKernelGGL((k_step_tpe<false, true>), dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);
-        else hipLaunchKernelGGL((k_step_tpe<false, false>), dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);
+        if (int r = check_launch()) return r;
+        if (!cfg->auto_reset) return 0;
+        // the deferred reset() of the envs that finished (lists written by the step)
+        const unsigned nb = (unsigned)((num_envs + 255) / 256);
+        if (tr) hipLaunchKernelGGL(k_reset_listed<true>, dim3(nb), dim3(BLOCK), 0, s, p);
+        else hipLaunchKernelGGL(k_reset_listed<false>, dim3(nb), dim3(BLOCK), 0, s, p);
         return check_launch();
     }
     LB_DISPATCH_SLICE(g.W, g.EPL, {

@@ -241,10 +241,12 @@ __device__ __forceinline__ void slice_reset(const Params& p, int64_t env, int la
             v.olat[k] = (float)v.lat0[k];
             v.ocpu[k] = (float)cpu;
         }
-        int64_t i = eidx(p, env, e);
-        p.lat0[i] = v.lat0[k];
-        p.emeta[i] = v.em[k];
-        p.edyn[i] = 0;
+        if (e < p.EP) {  // (the thread-per-env layout has no padding slots: EP = E)
+            const int64_t i = eidx(p, env, e);
+            p.lat0[i] = v.lat0[k];
+            p.emeta[i] = v.em[k];
+            p.edyn[i] = 0;
+        }
     }
     // topology (:331-338): symmetric, diag 1; the 4x4 zone block is all that is observable
     uint64_t topo = 0;
@@ -289,6 +291,33 @@ __global__ __launch_bounds__(BLOCK) void k_reset_slice(Params p) {
     slice_reset<W, EPL, TRACE>(p, env, lane, v);
     if (p.obs) slice_write_obs<W, EPL>(p, p.obs, env, lane, v);
     if (lane == 0) slice_store_scalars<EPL>(p, env, v);
+}
+
+// Deferred auto-reset of the thread-per-env step (k_step_tpe): reset() of the envs that
+// finished, read from the step's per-wave lists, with 16 lanes per env (the 24+ node draws
+// spread over lanes instead of one lane's serial chain).  Block b takes the lists of waves
+// 4b .. 4b + 3 (256 envs); slot s of its 16 slices resets their items s, s + 16, ...  Any
+// state layout: endpoint stores go through eidx.
+template <bool TRACE>
+__global__ __launch_bounds__(BLOCK) void k_reset_listed(Params p) {
+    constexpr int W = 16;
+    const int lane = threadIdx.x % W, slot = threadIdx.x / W;
+    const int64_t nseg = (p.B + 63) / 64, seg0 = (int64_t)blockIdx.x * 4;
+    int pre[5];
+    pre[0] = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) pre[k + 1] = pre[k] + (seg0 + k < nseg ? (int)p.rs_cnt[seg0 + k] : 0);
+    for (int i = slot; i < pre[4]; i += BLOCK / W) {
+        const int k = i < pre[1] ? 0 : (i < pre[2] ? 1 : (i < pre[3] ? 2 : 3));
+        const int64_t env = p.rs_ids[(seg0 + k) * 64 + (i - pre[k])];
+        SEnv<1> v;
+        v.t = p.t[env];
+        v.acc3 = p.acc3[env];
+        v.s = sc_unpack(p.sc[env]);
+        slice_reset<W, 1, TRACE>(p, env, lane, v);
+        if (p.obs) slice_write_obs<W, 1>(p, p.obs, env, lane, v);
+        if (lane == 0) slice_store_scalars<1>(p, env, v);
+    }
 }
 
 // step() (:403-513) fused with next_request(), get_state(), reward, done and auto-reset.

@@ -97,9 +97,11 @@ __device__ __forceinline__ void tpe_image_env(uint32_t* me, const TEnv& v, int f
 }
 
 // get_state() (:688-758) for the wave's envs: rows [zone, cap, cpu, topo, lat, rz, thr, dt],
-// plus the reject row [-1 x 5, rz, thr, dt].  flagged: only envs whose image flag is set.
+// plus the reject row [-1 x 5, rz, thr, dt].  which: COPY_ALL, or only the envs whose
+// image flag is set (COPY_FLAGGED) / clear (COPY_UNFLAGGED).
+enum { COPY_ALL = 0, COPY_FLAGGED = 1, COPY_UNFLAGGED = 2 };
 __device__ __forceinline__ void tpe_copy_out(const Params& p, float* out, const uint32_t* img,
-                                             int64_t env0, bool flagged) {
+                                             int64_t env0, int which) {
     const int lane = threadIdx.x & 63;
     const int P = 2 * p.R;  // float4 pieces per env (<= 18)
     const int G = 64 / P;   // envs per store instruction
@@ -111,7 +113,7 @@ __device__ __forceinline__ void tpe_copy_out(const Params& p, float* out, const 
     for (int el = eo; el < nenv; el += G) {
         const uint32_t* c = img + el * TPE_CW;
         const uint32_t w0 = c[0];
-        if (flagged && !(w0 & TPE_FLAG)) continue;
+        if (which != COPY_ALL && (which == COPY_FLAGGED) != ((w0 & TPE_FLAG) != 0)) continue;
         const int rz = (int)(w0 & 3);
         const float thr = (float)threshold((int)((w0 >> 2) & 7));
         const float dt = __uint_as_float(c[1]);
@@ -263,11 +265,16 @@ __global__ __launch_bounds__(NB) void k_reset_tpe(Params p) {
         tpe_store_scalars(p, env, v);
     }
     __syncthreads();
-    if (p.obs) tpe_copy_out(p, p.obs, img, env0, true);
+    if (p.obs) tpe_copy_out(p, p.obs, img, env0, COPY_FLAGGED);
 }
 
-// step() (:403-513) fused with next_request(), get_state(), reward, done and auto-reset.
-// RECOMPUTE (Philox mode, many envs): the scenario is redrawn instead of loaded.
+// step() (:403-513) fused with next_request(), get_state(), reward and done.  RECOMPUTE
+// (Philox mode, many envs): the scenario is redrawn instead of loaded.
+// VecEnv auto-reset: an env whose episode ends gets its terminal obs and episode-stats row
+// here; its reset() is deferred to k_reset_listed (lbk8s_slice.h), which runs next on the
+// stream over the compacted list of those envs (per wave: rs_cnt[wave] ids at
+// rs_ids[64 wave ..]).  Resetting inline made every wave holding one finishing env (~half
+// of them when episodes are staggered) carry reset()'s ~36 serial Philox blocks.
 template <bool TRACE, bool RECOMPUTE, int NB = BLOCK>
 __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
     __shared__ uint32_t lds[NB * TPE_CW];
@@ -422,23 +429,24 @@ __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
         if (p.reward) *(p.reward + env) = ((float)reward);
         if (p.done) p.done[env] = (uint8_t)done;
     }
-    tpe_image_env(me, v, done ? TPE_FLAG : 0);
-
-    // ---- VecEnv auto-reset: terminal obs + episode stats, then reset() (:290-400)
     const bool do_reset = done && p.auto_reset;
-    if (__syncthreads_or(do_reset)) {
-        if (p.term_obs) tpe_copy_out(p, p.term_obs, img, env0, true);
-        if (do_reset && p.ep_stats)
-            write_stats_row(p, p.ep_stats + env * LB_ST_K, v.s, v.acc2, v.acc3, v.total, v.sum_lat, v.sum_cpu);
-        __syncthreads();
+    tpe_image_env(me, v, do_reset ? TPE_FLAG : 0);
+
+    // ---- VecEnv auto-reset: terminal obs + episode stats; reset() itself is deferred
+    if (p.auto_reset) {
+        const uint64_t m = __ballot(do_reset);
         if (do_reset) {
-            tpe_reset<TRACE>(p, env, v, me);
-            tpe_image_env(me, v, 0);
+            p.rs_ids[env0 + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)env;
+            if (p.ep_stats)
+                write_stats_row(p, p.ep_stats + env * LB_ST_K, v.s, v.acc2, v.acc3, v.total, v.sum_lat, v.sum_cpu);
         }
+        if (lane == 0) p.rs_cnt[env0 >> 6] = (uint32_t)__popcll(m);
     }
     if (live) tpe_store_scalars(p, env, v);
     __syncthreads();
-    if (p.obs) tpe_copy_out(p, p.obs, img, env0, false);
+    if (p.term_obs && __syncthreads_or(do_reset)) tpe_copy_out(p, p.term_obs, img, env0, COPY_FLAGGED);
+    // finished envs' post-reset obs come from k_reset_listed
+    if (p.obs) tpe_copy_out(p, p.obs, img, env0, p.auto_reset ? COPY_UNFLAGGED : COPY_ALL);
 }
 
 }  // namespace lbk
