@@ -73,6 +73,7 @@ def parse(argv):
     ap.add_argument("--ring", type=int, default=16, help="rollout ring depth (obs slots)")
     ap.add_argument("--no-graph", action="store_true", help="launch every step eagerly")
     ap.add_argument("--lockstep", action="store_true", help="do not stagger episodes (all envs reset together)")
+    ap.add_argument("--geometry", default="auto", choices=("auto", "tpe", "slice"), help="E <= 8 kernel shape")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--plan-only", action="store_true", help="launcher + sharding + stats reduction, no GPU")
@@ -175,7 +176,7 @@ def main(argv=None):
     total = args.envs * (world if args.weak else 1)
     off, B = shard(total, rank, world)
     cfg_kwargs = CONFIGS[args.config]
-    env = LBVecEnv(B, device=dev, seed=0, env_id_offset=off, as_tensors=True, **cfg_kwargs)
+    env = LBVecEnv(B, device=dev, seed=0, env_id_offset=off, as_tensors=True, geometry=args.geometry, **cfg_kwargs)
     R = env.cfg.obs_rows
     L = env.cfg.episode_length
     T = max(1, args.ring)
@@ -268,7 +269,7 @@ def main(argv=None):
                                f"{env.cfg.reward_function}), {B} per GPU, obs ring T={T}, "
                                + ("lockstep" if args.lockstep else "staggered") + " episodes",
                    "envs_per_gpu": B, "total_envs": total, "scenario": args.config, "episode_length": L,
-                   "resets_in_window": resets, "graphs": graph is not None,
+                   "resets_in_window": resets, "graphs": graph is not None, "geometry": args.geometry,
                    "parallelism": f"env-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -532,7 +532,7 @@ int lb_step(void* state, const lb_config* cfg, int64_t num_envs, const int32_t* 
         if (int r = check_launch()) return r;
         if (!cfg->auto_reset) return 0;
         // the deferred reset() of the envs that finished (lists written by the step)
-        const unsigned nb = (unsigned)((num_envs + 255) / 256);
+        const unsigned nb = (unsigned)((num_envs + 64 * RS_SEG - 1) / (64 * RS_SEG));
         if (tr) hipLaunchKernelGGL(k_reset_listed<true>, dim3(nb), dim3(BLOCK), 0, s, p);
         else hipLaunchKernelGGL(k_reset_listed<false>, dim3(nb), dim3(BLOCK), 0, s, p);
         return check_launch();
