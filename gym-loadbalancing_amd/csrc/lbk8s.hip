@@ -604,6 +604,12 @@ unsigned ds_grid(int64_t groups) {
 
 template <int MODE>
 void ds_forward_launch(const DSParams& p, hipStream_t s) {
+    if constexpr (MODE != 1) {  // (the training forward covers R <= LB_DS_MAX_ELEMENTS)
+        if (p.R > LB_DS_MAX_ELEMENTS) {  // large sets: streamed in chunks, one env per wave
+            hipLaunchKernelGGL((k_deepsets_fwd_big<MODE>), dim3(ds_grid(p.B)), dim3(DS_BLOCK), 0, s, p);
+            return;
+        }
+    }
     // a wave takes P envs per iteration: P = 4 for R <= 16, 2 for R <= 32, else 1
     const int ts = (p.R + 15) / 16;
     const int P = ts == 1 ? 4 : (ts == 2 ? 2 : 1);
@@ -624,8 +630,8 @@ int lb_ds_forward(const float* frag, const float* obs, int64_t num_envs, int32_t
                   float* value_out, void* stream) {
     static_assert(DS_FLOATS == LB_DS_FRAG_FLOATS, "fragment layout and header disagree");
     if (!frag || !obs || num_envs < 1) return fail("frag/obs NULL or num_envs < 1");
-    if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS)
-        return fail("num_elements must be in [1, 80] (LB_DS_MAX_ELEMENTS)");
+    if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS_FWD)
+        return fail("num_elements must be in [1, 257] (LB_DS_MAX_ELEMENTS_FWD)");
     if (!logits_out && !value_out) return 0;
     DSParams p{obs, frag, logits_out, value_out, num_envs, num_elements, logits_out != nullptr, value_out != nullptr,
                nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -636,8 +642,8 @@ int lb_ds_forward(const float* frag, const float* obs, int64_t num_envs, int32_t
 int lb_ds_q_argmax(const float* frag, const float* obs, int64_t num_envs, int32_t num_elements, const uint8_t* masks,
                    float* q_out, int32_t* actions_out, void* stream) {
     if (!frag || !obs || !actions_out || num_envs < 1) return fail("frag/obs/actions_out NULL or num_envs < 1");
-    if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS)
-        return fail("num_elements must be in [1, 80] (LB_DS_MAX_ELEMENTS)");
+    if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS_FWD)
+        return fail("num_elements must be in [1, 257] (LB_DS_MAX_ELEMENTS_FWD)");
     DSParams p{obs, frag, q_out, nullptr, num_envs, num_elements, 1, 0, nullptr, nullptr, nullptr, actions_out, masks};
     ds_forward_launch<2>(p, (hipStream_t)stream);
     return check_launch();

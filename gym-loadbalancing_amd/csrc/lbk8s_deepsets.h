@@ -374,6 +374,187 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
     }
 }
 
+// ---- large sets (LB_DS_MAX_ELEMENTS < R <= LB_DS_MAX_ELEMENTS_FWD) ------------------------
+// One env per wave iteration; the set is streamed in chunks of DS_CT 16-row tiles (32 elements).  A layer
+// needs the set-wise max of its input, so each layer's max is one pass over the chunks that
+// recomputes the earlier layers of the chunk: nothing per element leaves registers, at the
+// price of layer 1 three times and layer 2 twice for the actor (R up to 257: E <= 256 with
+// the reject row).  Same fragments, same per-element math as k_deepsets_fwd.
+constexpr int DS_CT = 2;
+
+template <int KS>
+__device__ __forceinline__ void chunk_max_acc(const float (&h)[DS_CT][KS], float (&acc)[KS], int row0, int col, int R) {
+#pragma unroll
+    for (int t = 0; t < DS_CT; ++t)
+        if (row0 + 16 * t + col < R)
+#pragma unroll
+            for (int k = 0; k < KS; ++k) acc[k] = max2(acc[k], h[t][k]);
+}
+
+__device__ __forceinline__ void load_obs_chunk(const float* x, int row0, int R, int col, int grp, float (&h0)[DS_CT][2]) {
+#pragma unroll
+    for (int t = 0; t < DS_CT; ++t) {
+        const int row = row0 + 16 * t + col;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) h0[t][kk] = row < R ? x[row * 8 + 4 * kk + grp] : 0.f;
+    }
+}
+
+// MODE 0: logits / value; 2: Q values and the masked greedy action (actor only)
+template <int MODE>
+__global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd_big(DSParams p) {
+    constexpr bool ARGMAX = MODE == 2;
+    __shared__ __attribute__((aligned(16))) float W[DS_LDS_FLOATS];
+    const int nstage = (ARGMAX || !p.critic) ? DS_C1L : DS_FLOATS;
+    for (int i = threadIdx.x * 4; i < nstage; i += DS_BLOCK * 4)
+        *reinterpret_cast<float4*>(W + i) = *reinterpret_cast<const float4*>(p.wfrag + i);
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * (DS_BLOCK / 64) + (threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * (DS_BLOCK / 64);
+    const int R = p.R;
+    const int col = lane & 15, grp = lane >> 4;
+    const int nch = (R + 16 * DS_CT - 1) / (16 * DS_CT);
+    for (int64_t env = wave; env < p.B; env += nwaves) {
+        const float* x = p.obs + env * (int64_t)R * 8;
+        // the weight fragments are re-read from LDS in every chunk: an opaque base pointer
+        // per chunk keeps the compiler from hoisting KiBs of loop-invariant loads into
+        // registers (which spilled to scratch)
+        // (an opaque 32-bit offset into the shared array keeps the loads ds_reads)
+        float h0[DS_CT][2], h1[DS_CT][16], h2[DS_CT][16];
+        float m0[2] = {-INFINITY, -INFINITY};
+        for (int c = 0; c < nch; ++c) {
+            load_obs_chunk(x, 16 * DS_CT * c, R, col, grp, h0);
+            chunk_max_acc<2>(h0, m0, 16 * DS_CT * c, col, R);
+        }
+        row_reduce<true>(m0);
+        if (p.actor) {
+            float m1[16], m2[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) m1[k] = m2[k] = -INFINITY;
+            for (int c = 0; c < nch; ++c) {
+                uint32_t wo = 0;
+                asm volatile("" : "+s"(wo));
+                const float* Wc = W + wo;
+                load_obs_chunk(x, 16 * DS_CT * c, R, col, grp, h0);
+                eq_layer<DS_CT, 1, 2, 1>(Wc + DS_A1L, Wc + DS_A1G, h0, m0, h1, lane);
+                chunk_max_acc<16>(h1, m1, 16 * DS_CT * c, col, R);
+            }
+            row_reduce<true>(m1);
+            for (int c = 0; c < nch; ++c) {
+                uint32_t wo = 0;
+                asm volatile("" : "+s"(wo));
+                const float* Wc = W + wo;
+                load_obs_chunk(x, 16 * DS_CT * c, R, col, grp, h0);
+                eq_layer<DS_CT, 1, 2, 1>(Wc + DS_A1L, Wc + DS_A1G, h0, m0, h1, lane);
+                eq_layer<DS_CT, 1, 16, 2>(Wc + DS_A2L, Wc + DS_A2G, h1, m1, h2, lane);
+                chunk_max_acc<16>(h2, m2, 16 * DS_CT * c, col, R);
+            }
+            row_reduce<true>(m2);
+            const float* G = W + DS_A3G + 16 * grp;
+            float gl = 0.f;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) gl += G[k * 64] * m2[k];
+            gl += __shfl_xor(gl, 16);
+            gl += __shfl_xor(gl, 32);
+            float best = -INFINITY, brow = 1e9f;
+            for (int c = 0; c < nch; ++c) {
+                uint32_t wo = 0;
+                asm volatile("" : "+s"(wo));
+                const float* Wc = W + wo;
+                load_obs_chunk(x, 16 * DS_CT * c, R, col, grp, h0);
+                eq_layer<DS_CT, 1, 2, 1>(Wc + DS_A1L, Wc + DS_A1G, h0, m0, h1, lane);
+                eq_layer<DS_CT, 1, 16, 2>(Wc + DS_A2L, Wc + DS_A2G, h1, m1, h2, lane);
+#pragma unroll
+                for (int t = 0; t < DS_CT; ++t) {
+                    float v = 0.f;
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) v += Wc[DS_A3L + 16 * grp + k * 64] * h2[t][k];
+                    v += __shfl_xor(v, 16);
+                    v += __shfl_xor(v, 32);
+                    const int row = 16 * DS_CT * c + 16 * t + col;
+                    if (row >= R) continue;
+                    if (grp == 0 && p.logits) p.logits[env * R + row] = gl + v;
+                    if (ARGMAX) {
+                        const float q = (!p.masks || p.masks[env * R + row]) ? gl + v : -1e8f;
+                        if (q > best) {  // rows ascend: the first maximum of this lane wins
+                            best = q;
+                            brow = (float)row;
+                        }
+                    }
+                }
+            }
+            if (ARGMAX) {
+                float m[1] = {best};
+                row_reduce<true>(m);
+                float cc[1] = {best == m[0] ? -brow : -1e9f};
+                row_reduce<true>(cc);
+                if (lane == 0) p.actions[env] = (int32_t)(-cc[0]);
+            }
+        }
+        if (ARGMAX || !p.critic) continue;
+        // critic: the max of c1, then the max and the sum of c2, then layer 3 / rho as above
+        float mc1[16], mc2[16], sm[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            mc1[k] = mc2[k] = -INFINITY;
+            sm[k] = 0.f;
+        }
+        for (int c = 0; c < nch; ++c) {
+            uint32_t wo = 0;
+            asm volatile("" : "+s"(wo));
+            const float* Wc = W + wo;
+            load_obs_chunk(x, 16 * DS_CT * c, R, col, grp, h0);
+            eq_layer<DS_CT, 1, 2, 2>(Wc + DS_C1L, Wc + DS_C1G, h0, m0, h1, lane);
+            chunk_max_acc<16>(h1, mc1, 16 * DS_CT * c, col, R);
+        }
+        row_reduce<true>(mc1);
+        for (int c = 0; c < nch; ++c) {
+            uint32_t wo = 0;
+            asm volatile("" : "+s"(wo));
+            const float* Wc = W + wo;
+            load_obs_chunk(x, 16 * DS_CT * c, R, col, grp, h0);
+            eq_layer<DS_CT, 1, 2, 2>(Wc + DS_C1L, Wc + DS_C1G, h0, m0, h1, lane);
+            eq_layer<DS_CT, 1, 16, 2>(Wc + DS_C2L, Wc + DS_C2G, h1, mc1, h2, lane);
+            chunk_max_acc<16>(h2, mc2, 16 * DS_CT * c, col, R);
+#pragma unroll
+            for (int t = 0; t < DS_CT; ++t)
+                if (16 * DS_CT * c + 16 * t + col < R)
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) sm[k] += h2[t][k];
+        }
+        row_reduce<true>(mc2);
+        row_reduce<false>(sm);
+        const float invR = 1.0f / (float)R;
+        float mean[16];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            dsf4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) acc = mfma4(W[DS_C3G + (nt * 16 + k) * 64 + lane], mc2[k], acc);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) acc = mfma4(W[DS_C3L + (nt * 16 + k) * 64 + lane], sm[k] * invR, acc);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) mean[4 * nt + i] = acc[i];
+        }
+        float r1[16];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            dsf4 acc;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[i] = W[DS_R1B + 16 * nt + 4 * grp + i];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) acc = mfma4(W[DS_R1W + (nt * 16 + k) * 64 + lane], mean[k], acc);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) r1[4 * nt + i] = act_elu(acc[i]);
+        }
+        dsf4 v = {W[DS_R2B], 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v = mfma4(W[DS_R2W + k * 64 + lane], r1[k], v);
+        if (lane == 0) p.value[env] = v[0];
+    }
+}
+
 // lb_ds_pack: one thread per fragment float
 struct DSPackRegion {
     int off, nout, kin, ks;

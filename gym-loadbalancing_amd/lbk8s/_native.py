@@ -53,7 +53,8 @@ class LBDSWeightsC(C.Structure):
 
 
 LB_DS_FRAG_FLOATS = 33860
-LB_DS_MAX_ELEMENTS = 80
+LB_DS_MAX_ELEMENTS = 80       # training kernels
+LB_DS_MAX_ELEMENTS_FWD = 257  # inference forward / greedy argmax
 LB_DS_BWD_FLOATS = 24704
 LB_DS_SETVEC_FLOATS = 648
 LB_DS_WGRAD_FLOATS = 4608

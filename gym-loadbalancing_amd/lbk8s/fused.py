@@ -12,8 +12,10 @@ parameter's version counter moves (every optimizer step bumps it), so callers ne
 repack by hand.
 
 Training runs the fused training kernels (lbk8s/fused_train.py), which use the same image.
-Inputs the kernel does not cover (not on a HIP device, R > 80, non-reference widths) run
-the same torch modules on the same device; `require=True` turns that into an error instead.
+The forward covers R <= 257 (every env the C ABI accepts: E <= 256 plus the reject row;
+above 80 elements the kernel streams the set in 32-element chunks).  Inputs it does not cover (not on
+a HIP device, non-reference widths) run the same torch modules on the same device;
+`require=True` turns that into an error instead.
 """
 import ctypes as C
 import weakref
@@ -54,7 +56,7 @@ def _weights_struct(actor_net, critic):
 
 
 def _geometry_ok(actor_net, x):
-    return (x.is_cuda and x.dim() == 3 and x.shape[-1] == 8 and 1 <= x.shape[1] <= _native.LB_DS_MAX_ELEMENTS
+    return (x.is_cuda and x.dim() == 3 and x.shape[-1] == 8 and 1 <= x.shape[1] <= _native.LB_DS_MAX_ELEMENTS_FWD
             and actor_net[0].Lambda.weight.shape == (64, 8) and actor_net[2].Lambda.weight.shape == (64, 64))
 
 

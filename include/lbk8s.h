@@ -179,13 +179,17 @@ int lb_status(const void* state, const lb_config* cfg, int64_t num_envs, uint32_
  * EquivariantLayer, EquivariantDeepSet actor, InvariantDeepSet critic; DQN's Q network is
  * the same equivariant stack, envs/deep_sets_agent_dqn.py:10-42).  Here one launch reads
  * an env's [R, 8] observation once and writes its R actor outputs and its critic value.
- * Only the reference geometry is supported: 8 input channels, 64 hidden, R <= 80.
+ * Only the reference geometry is supported: 8 input channels, 64 hidden.  Inference
+ * (lb_ds_forward, lb_ds_q_argmax) takes R <= 257 (E <= 256 plus the reject row; above 80
+ * the set is streamed through the kernel in 32-element chunks); the training entry points
+ * take R <= 80.
  * Weights are the torch parameters as they are (nn.Linear layout [out][in], f32, device);
  * lb_ds_pack rearranges them into the kernel's fragment order (LB_DS_FRAG_FLOATS floats),
  * to be redone after every optimizer step.  A NULL critic pointer set packs an actor-only
  * image (DQN); lb_ds_forward then must be called with value_out == NULL. */
 #define LB_DS_FRAG_FLOATS 33860
-#define LB_DS_MAX_ELEMENTS 80
+#define LB_DS_MAX_ELEMENTS 80       /* training forward / backward */
+#define LB_DS_MAX_ELEMENTS_FWD 257  /* inference forward, greedy argmax */
 
 typedef struct lb_ds_weights {
     const float* actor_lambda[3];  /* actor.net.{0,2,4}.Lambda.weight [64,8] [64,64] [1,64]  */
@@ -202,7 +206,7 @@ typedef struct lb_ds_weights {
 int lb_ds_pack(const lb_ds_weights* w, float* frag_out, void* stream);
 
 /* obs [B, R, 8] f32 -> logits_out [B, R] f32 (actor / Q values; NULL = skip) and
- * value_out [B] f32 (critic; NULL = skip).  1 <= R <= LB_DS_MAX_ELEMENTS. */
+ * value_out [B] f32 (critic; NULL = skip).  1 <= R <= LB_DS_MAX_ELEMENTS_FWD. */
 int lb_ds_forward(const float* frag, const float* obs, int64_t num_envs, int32_t num_elements,
                   float* logits_out, float* value_out, void* stream);
 

@@ -104,8 +104,11 @@ def ppo_minibatch_loss(agent, mb, clip_coef=0.2, ent_coef=0.001, vf_coef=0.5, no
     return loss, pg_loss, v_loss, entropy_loss, approx_kl
 
 
-def gen_ppo(ds):
-    obs = torch.from_numpy(real_obs("default_naive", 100))
+def gen_ppo(ds, fixture="default_naive", n=100, out_name="nn_ppo_update.npz", random_masks=False):
+    """One PPO minibatch update.  The E = 64 variant (config 4's geometry, R = 65, 256 sets,
+    ~10% of the actions masked out, the taken action always valid) pins the fused training
+    kernels and the loss head at the shape the config-4 learner runs."""
+    obs = torch.from_numpy(real_obs(fixture, n))
     B, R, _ = obs.shape
     torch.manual_seed(2)
     agent = ds.DeepSetAgent(_Envs(R, R))
@@ -114,6 +117,9 @@ def gen_ppo(ds):
     with torch.no_grad():
         actions, logprobs, _, values = agent.get_action_and_value(obs)
     masks = torch.ones((B, R), dtype=torch.bool)
+    if random_masks:
+        masks = torch.rand((B, R), generator=g) > 0.1
+        masks[torch.arange(B), actions] = True
     advantages = torch.randn(B, generator=g)
     returns = values.view(-1) + torch.randn(B, generator=g) * 0.5
     mb = dict(obs=obs, actions=actions.float(), logprobs=logprobs + 0.05 * torch.randn(B, generator=g),
@@ -131,7 +137,7 @@ def gen_ppo(ds):
     out.update(sd_arrays(agent, "after__"))
     out.update(loss=loss.item(), pg_loss=pg.item(), v_loss=vl.item(), entropy_loss=ent.item(),
                approx_kl=kl.item(), grad_norm=gnorm.item(), ent_coef=0.001, clip_coef=0.2, vf_coef=0.5)
-    np.savez_compressed(os.path.join(HERE, "nn_ppo_update.npz"), **out)
+    np.savez_compressed(os.path.join(HERE, out_name), **out)
 
 
 def gen_dqn(dqn_mod):
@@ -183,6 +189,7 @@ def main():
     for name, fx in (("e6", "cfg1_multi"), ("e8", "default_naive"), ("e64", "e64_multi")):
         man[name] = gen_forward(ds, dqn_mod, name, fx)
     gen_ppo(ds)
+    gen_ppo(ds, "e64_multi", 256, "nn_ppo_update_e64.npz", random_masks=True)
     gen_dqn(dqn_mod)
     man["torch"] = torch.__version__
     with open(os.path.join(HERE, "MANIFEST_nn.json"), "w") as f:

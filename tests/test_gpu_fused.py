@@ -42,7 +42,7 @@ def test_fused_forward_matches_reference(name):
     assert (qm.argmax(1).cpu().numpy() == d["q_mode_masked"]).all()
 
 
-@pytest.mark.parametrize("R", [1, 2, 7, 9, 15, 16, 17, 31, 32, 33, 48, 49, 64, 65, 79, 80])
+@pytest.mark.parametrize("R", [1, 2, 7, 9, 15, 16, 17, 31, 32, 33, 48, 49, 64, 65, 79, 80, 81, 128, 129, 181, 257])
 def test_fused_forward_all_set_sizes(R):
     from lbk8s import fused
     from lbk8s.deepsets import DeepSetAgent
@@ -98,15 +98,15 @@ def test_fused_rejects_uncovered_inputs():
     from lbk8s import fused
     from lbk8s.deepsets import DeepSetAgent
     agent = DeepSetAgent(8).cuda()
-    x = torch.randn(4, 81, 8, device="cuda")
+    x = torch.randn(4, 258, 8, device="cuda")
     with pytest.raises(RuntimeError):
         fused.deepsets_forward(agent, x, require=True)
     logits, value = fused.deepsets_forward(agent, x)  # torch modules on the same device
-    assert logits.shape == (4, 81) and value.shape == (4,) and logits.is_cuda
+    assert logits.shape == (4, 258) and value.shape == (4,) and logits.is_cuda
     np.testing.assert_array_equal(np.isfinite(logits.cpu().numpy()), True)
 
 
-@pytest.mark.parametrize("R", [7, 9, 20, 65])
+@pytest.mark.parametrize("R", [7, 9, 20, 65, 100, 181])
 def test_fused_q_argmax(R):
     """lb_ds_q_argmax: the Q forward with the masked greedy action fused
     (dqn_deepset.py:134-142: argmax of where(mask, q, -1e8), first index on ties)."""

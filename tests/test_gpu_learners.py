@@ -57,3 +57,52 @@ def test_ppo_graph_update_matches_eager():
         res.append([p.detach().clone() for p in algo.agent.parameters()])
     for a, b in zip(*res):
         torch.testing.assert_close(b, a, rtol=1e-4, atol=2e-6)
+
+
+def test_ppo_config4_end_to_end_graph_step_matches_reference():
+    """Config 4 end to end: PPO_DeepSets on 512 E=64 multi-reward envs (R = 65), T = 8,
+    graphs on: a rollout + update runs, then the captured minibatch step (fused forward,
+    fused loss head, fused backward, clip_grad_norm, Adam) is replayed on the reference's
+    own R = 65 minibatch (tests/golden/nn_ppo_update_e64.npz, ppo_deepset.py:216-267 through
+    envs/deep_sets_agent_original.py) from the reference's initial weights: gradients,
+    their clipped norm and the Adam step must match."""
+    import numpy as np
+
+    from lbk8s import LBVecEnv
+    from lbk8s.ppo import PPO_DeepSets
+    from nn_helpers import close, load_nn, state_dict_from
+    from test_nn_golden import check_adam_step
+    d = load_nn("nn_ppo_update_e64")
+    S = d["obs"].shape[0]  # 256 sets = one minibatch of 512 envs x 8 steps / 16
+    env = LBVecEnv(512, seed=9, as_tensors=True, num_endpoints=64, reward_function="multi",
+                   latency_weight=1.0, cpu_weight=0.0, gini_weight=0.0)
+    logs = []
+    algo = PPO_DeepSets(env, num_steps=8, n_minibatches=16, update_epochs=1, ent_coef=float(d["ent_coef"]), seed=2,
+                        log_fn=logs.append)
+    assert algo.use_graphs and algo.minibatch_size == S and env.observation_space.shape == (65, 8)
+    algo.learn(total_timesteps=512 * 8)
+    assert len(logs) == 1 and all(math.isfinite(logs[0][k]) for k in ("loss", "pg_loss", "v_loss", "entropy"))
+    assert algo._mb_graphs is not None
+    # the reference's minibatch and initial weights into the captured step's buffers
+    with torch.no_grad():
+        algo.agent.load_state_dict(state_dict_from(d, "init__"))
+        for st in algo.optimizer.state.values():
+            for v in st.values():
+                if isinstance(v, torch.Tensor):
+                    v.zero_()
+        names = ("obs", "actions", "logprobs", "masks", "advantages", "returns", "values")
+        for buf, k in zip(algo._static, names):
+            buf.copy_(torch.from_numpy(np.asarray(d[k])).to(buf.device, buf.dtype))
+    from lbk8s import fused
+    fused.invalidate(algo.agent)
+    algo._replay()
+    torch.cuda.synchronize()
+    loss = algo._static_out[0]
+    close(loss, d["loss"], rtol=1e-4, atol=2e-5, what="loss")
+    gmax = max(np.abs(d["grad__" + n.replace(".", "__")]).max() for n, _ in algo.agent.named_parameters())
+    gn = float(d["grad_norm"])
+    scale = min(1.0, 0.5 / (gn + 1e-6))  # clip_grad_norm_ already scaled the replayed gradients
+    for n, p in algo.agent.named_parameters():
+        close(p.grad / scale, d["grad__" + n.replace(".", "__")], what="grad " + n, rtol=1e-3,
+              atol=max(2e-4, 1e-5 * gmax))
+    check_adam_step(algo.agent, d, gmax, "cuda")

@@ -71,10 +71,13 @@ def test_deepsets_forward_matches_reference(name, device):
 
 
 @pytest.mark.parametrize("device", DEVICES)
-def test_ppo_minibatch_update_matches_reference(device):
+@pytest.mark.parametrize("golden", ["nn_ppo_update", "nn_ppo_update_e64"])
+def test_ppo_minibatch_update_matches_reference(device, golden):
+    """R = 9 (100 sets) and config 4's R = 65 (256 sets, masked actions): on the GPU the
+    fused training kernels and the fused loss head run."""
     from lbk8s.deepsets import DeepSetAgent
     from lbk8s.ppo import ppo_loss
-    d = load_nn("nn_ppo_update")
+    d = load_nn(golden)
     agent = DeepSetAgent(8).to(device)
     agent.load_state_dict(state_dict_from(d, "init__"))
     f = lambda k, dt=torch.float32: torch.from_numpy(np.asarray(d[k])).to(device, dt)  # noqa: E731
