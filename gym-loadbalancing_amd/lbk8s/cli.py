@@ -58,6 +58,8 @@ def build_parser():
     p.add_argument("--num_envs", default=8, type=int, help="parallel envs on the GPU (reference: 8 workers)")
     p.add_argument("--no_training", action="store_true", help="skip training (--training is always on)")
     p.add_argument("--test_episodes", default=1, type=int, help="episodes played side by side by --testing")
+    p.add_argument("--test_sequential", action="store_true",
+                   help="--testing plays the episodes one after another on one env, as run_test_deepset.py")
     p.add_argument("--device", default="cuda")
     p.add_argument("--seed", default=0, type=int, help="Philox seed of the envs")
     p.add_argument("--nproc", default=1, type=int, help="GPUs (ranks) to train on, one process each")
@@ -141,10 +143,15 @@ def main(argv=None):
             if rank != 0:
                 return result
     if args.testing:
-        from .evaluate import load_agent, run_test
+        from .evaluate import load_agent, run_sequential, run_test
         agent = load_agent(args.test_path, "ppo" if alg == "ppo_deepsets" else "dqn", device=args.device)
-        res = run_test(agent, n_episodes=args.test_episodes, seed=args.seed, device=args.device,
-                       **env_kwargs(args.rejection, num_endpoints, num_zones, num_nodes, reward))
+        kw = env_kwargs(args.rejection, num_endpoints, num_zones, num_nodes, reward)
+        if args.test_sequential:
+            from .vec_env import LBVecEnv
+            env = LBVecEnv(1, device=args.device, seed=args.seed, as_tensors=True, **kw)
+            res = run_sequential(agent, args.test_episodes, env)
+        else:
+            res = run_test(agent, n_episodes=args.test_episodes, seed=args.seed, device=args.device, **kw)
         result["test_returns"] = [float(r) for r in res["r"]]
     print(json.dumps(result))
     return result

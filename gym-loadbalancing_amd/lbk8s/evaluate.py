@@ -6,11 +6,17 @@ and plays `n_episodes` episodes on ONE env, one after the other, with determinis
 masked argmax actions (`agent.predict(obs, action_mask)`), while VecMonitor writes the
 per-episode return and the info keywords.
 
-Here the episodes run side by side: `n_episodes` envs on the device, one vector step per
-time step: logits (PPO actor) or Q values (DQN) from the fused forward kernel, masked
-argmax, the fused env step.  Auto-reset is off, so every env plays exactly one episode
-(episode_length steps).  Episode i is the scenario of global env id `env_id_offset + i`
-(Philox), so any single episode can be replayed alone.
+Two forms:
+* run_test: the episodes run side by side: `n_episodes` envs on the device, one vector
+  step per time step: logits (PPO actor) or Q values (DQN) from the fused forward kernel,
+  masked argmax, the fused env step.  Auto-reset is off, so every env plays exactly one
+  episode (episode_length steps).  Episode i is the scenario of global env id
+  `env_id_offset + i` (Philox), so any single episode can be replayed alone.
+* run_sequential: the reference loop as written — ONE env, episodes one after another,
+  DummyVecEnv's auto-reset on done followed by the loop's own reset() (so the auto-reset's
+  scenario is drawn and discarded), VecMonitor's float32 episode return.  Pinned by
+  fixtures recorded from the reference env + the reference networks
+  (tests/golden/gen_golden_eval.py) replayed in trace mode.
 """
 import csv
 import time
@@ -71,6 +77,56 @@ def run_test(agent, n_episodes=2000, seed=42, env_id_offset=0, device="cuda", mo
     if monitor_path is not None:
         write_monitor_csv(monitor_path, out, INFO_KEYS[:12])
     return out
+
+
+@torch.no_grad()
+def run_sequential(agent, n_episodes, env, draws=None, monitor_path=None, info_keywords=INFO_KEYS):
+    """run_test_deepset.py:83-98 on a one-env LBVecEnv (auto_reset on, as DummyVecEnv):
+
+        for episode: obs = envs.reset(); mask = env_method("action_masks")
+                     while not done: obs, r, dones, info = envs.step(agent.predict(obs, mask))
+
+    draws: None (Philox) or, for an env in trace mode, an object whose next_reset() /
+    next_step() return the reference's draws for the next reset() / step() in call order
+    (the step that ends an episode also consumes the auto-reset's).  Returns per-step
+    "actions" / "rewards" / "dones" and per-episode "r" (VecMonitor's float32 return), "l",
+    "total_reward" (float64) and the final info's keys."""
+    if env.num_envs != 1 or not env.auto_reset:
+        raise ValueError("run_sequential plays one env with auto-reset (DummyVecEnv of one env)")
+    L = env.cfg.episode_length
+    out = {k: [] for k in ("actions", "rewards", "dones", "r", "l", "total_reward")}
+    for k in info_keywords:
+        out[k] = []
+    for _ in range(n_episodes):
+        obs = env.reset(trace=draws.next_reset() if draws is not None else None)
+        obs = torch.as_tensor(obs, device=env.device)
+        masks = env.action_masks()
+        done, ret32, length = False, np.float32(0.0), 0
+        while not done:
+            a = greedy_actions(agent, obs, masks)
+            st = draws.next_step() if draws is not None else None
+            rt = draws.next_reset() if (draws is not None and length + 1 == L) else None
+            obs, rew, dones, infos = env.step(a, trace=st, reset_trace=rt)
+            obs = torch.as_tensor(obs, device=env.device)
+            r = float(np.asarray(rew.cpu() if isinstance(rew, torch.Tensor) else rew)[0])
+            done = bool(np.asarray(dones.cpu() if isinstance(dones, torch.Tensor) else dones)[0])
+            ret32 = np.float32(ret32 + np.float32(r))
+            length += 1
+            out["actions"].append(int(a[0]))
+            out["rewards"].append(r)
+            out["dones"].append(done)
+            if done:
+                info = infos[0]
+                out["r"].append(float(ret32))
+                out["l"].append(length)
+                out["total_reward"].append(float(env._host_ep_stats()[0, ST_RETURN]))
+                for k in info_keywords:
+                    out[k].append(info[k])
+    res = {k: np.asarray(v) for k, v in out.items()}
+    if monitor_path is not None:
+        res["wall_s"] = 0.0
+        write_monitor_csv(monitor_path, res, info_keywords)
+    return res
 
 
 def write_monitor_csv(path, res, info_keywords):
