@@ -17,9 +17,9 @@ def pytest_configure(config):
 
 
 def golden_names(prefix=""):
-    """Env-trajectory fixtures (the nn_* files hold network / learner goldens)."""
+    """Env-trajectory fixtures (nn_* hold network / learner goldens, eval_* evaluation loops)."""
     return sorted(f[:-4] for f in os.listdir(GOLDEN)
-                  if f.endswith(".npz") and f.startswith(prefix) and not f.startswith("nn_"))
+                  if f.endswith(".npz") and f.startswith(prefix) and not f.startswith(("nn_", "eval_")))
 
 
 @pytest.fixture(scope="session")
