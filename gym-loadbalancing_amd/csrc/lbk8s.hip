@@ -545,6 +545,45 @@ int lb_step(void* state, const lb_config* cfg, int64_t num_envs, const int32_t* 
     return check_launch();
 }
 
+int lb_rollout(void* state, const lb_config* cfg, int64_t num_envs, int32_t policy, int32_t steps,
+               float* obs_out, float* reward_out, uint8_t* done_out, int32_t* actions_out,
+               float* terminal_obs_out, double* ep_stats_out, void* stream) {
+    if (int r = validate(cfg)) return r;
+    if (!state || num_envs < 1) return fail("state NULL or num_envs < 1");
+    if (cfg->rng_mode != LB_RNG_PHILOX) return fail("lb_rollout draws in Philox mode only");
+    if (policy < 0 || policy > LB_POLICY_RANDOM) return fail("unknown policy kind");
+    if (steps < 0) return fail("steps must be >= 0");
+    Geo g = geometry(cfg, num_envs);
+    hipStream_t s = (hipStream_t)stream;
+    if (g.tpe) {  // thread-per-env layout: K policy + step launches
+        if (policy != LB_POLICY_RANDOM && !actions_out)
+            return fail("lb_rollout on the thread-per-env layout needs actions_out for a greedy policy");
+        const int64_t R = cfg->num_endpoints + (cfg->rejection_allowed ? 1 : 0);
+        for (int k = 0; k < steps; ++k) {
+            int32_t* act = actions_out ? actions_out + k * num_envs : nullptr;
+            if (act)
+                if (int r = lb_policy(state, cfg, num_envs, policy, act, stream)) return r;
+            if (int r = lb_step(state, cfg, num_envs, act, obs_out ? obs_out + k * num_envs * R * 8 : nullptr,
+                                reward_out ? reward_out + k * num_envs : nullptr,
+                                done_out ? done_out + k * num_envs : nullptr, terminal_obs_out, ep_stats_out,
+                                nullptr, stream))
+                return r;
+        }
+        return 0;
+    }
+    Params p = make_params(state, cfg, num_envs);
+    p.obs = obs_out;
+    p.reward = reward_out;
+    p.done = done_out;
+    p.term_obs = terminal_obs_out;
+    p.ep_stats = ep_stats_out;
+    LB_DISPATCH_SLICE(g.W, g.EPL, {
+        hipLaunchKernelGGL((k_rollout_slice<W, EPL>), dim3(slice_blocks(num_envs, W)), dim3(BLOCK), 0, s, p,
+                           (int)policy, (int)steps, actions_out);
+    });
+    return check_launch();
+}
+
 int lb_policy(const void* state, const lb_config* cfg, int64_t num_envs, int32_t kind,
               int32_t* actions_out, void* stream) {
     if (int r = validate(cfg)) return r;

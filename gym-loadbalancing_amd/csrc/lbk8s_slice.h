@@ -327,18 +327,14 @@ __global__ __launch_bounds__(BLOCK) void k_reset_listed(Params p) {
     }
 }
 
-// step() (:403-513) fused with next_request(), get_state(), reward, done and auto-reset.
-template <int W, int EPL, bool TRACE>
-__global__ __launch_bounds__(BLOCK) void k_step_slice(Params p) {
-    const int lane = threadIdx.x % W;
-    const int64_t env = (int64_t)blockIdx.x * (BLOCK / W) + threadIdx.x / W;
-    if (env >= p.B) return;
+// One step() (:403-513) of the slice's env held in registers, fused with next_request(),
+// get_state(), reward, done and auto-reset: action a in, obs / reward / done of this step
+// out (NULL = skip).  STORE_ED: write the changed history counters back at once (the
+// single-step kernel); a multi-step kernel keeps them in registers and stores them at the end.
+template <int W, int EPL, bool TRACE, bool STORE_ED>
+__device__ __forceinline__ void slice_step_body(const Params& p, int64_t env, int lane, SEnv<EPL>& v, int a,
+                                                float* obs_out, float* reward_out, uint8_t* done_out) {
     const int E = p.E;
-    // ---- phase 0: independent loads (state + action)
-    SEnv<EPL> v;
-    slice_load<W, EPL>(p, env, lane, v);
-    const int a = p.actions ? p.actions[env] : random_action(p, env, v.acc3, v.s.step);  // fused random policy
-
     // ---- phase 1: decode, then every table lookup the step needs, issued together
     v.s.step = v.s.step < 0xFFFF ? v.s.step + 1 : 0xFFFF;
     const bool accept = a >= -E && a < E;
@@ -424,22 +420,93 @@ __global__ __launch_bounds__(BLOCK) void k_step_slice(Params p) {
     slice_next_request<W, TRACE, EPL>(p, env, lane, false, v);
     const bool done = v.s.step == p.L;
     if (lane == 0) {
-        if (p.reward) p.reward[env] = (float)reward;
-        if (p.done) p.done[env] = (uint8_t)done;
+        if (reward_out) reward_out[env] = (float)reward;
+        if (done_out) done_out[env] = (uint8_t)done;
     }
     if (done && p.auto_reset) {
         if (p.term_obs) slice_write_obs<W, EPL>(p, p.term_obs, env, lane, v);
         if (p.ep_stats && lane == 0)
             write_stats_row(p, p.ep_stats + env * LB_ST_K, v.s, v.acc2, v.acc3, v.total, v.sum_lat, v.sum_cpu);
         slice_reset<W, EPL, TRACE>(p, env, lane, v);
-    } else if (accept) {
+    } else if (STORE_ED && accept) {
 #pragma unroll
         for (int k = 0; k < EPL; ++k) {
             int e = lane + k * W;
             if (e == ai || e == oA) p.edyn[eidx(p, env, e)] = v.ed[k];
         }
     }
-    if (p.obs) slice_write_obs<W, EPL>(p, p.obs, env, lane, v);
+    if (obs_out) slice_write_obs<W, EPL>(p, obs_out, env, lane, v);
+}
+
+// step() (:403-513) fused with next_request(), get_state(), reward, done and auto-reset.
+template <int W, int EPL, bool TRACE>
+__global__ __launch_bounds__(BLOCK) void k_step_slice(Params p) {
+    const int lane = threadIdx.x % W;
+    const int64_t env = (int64_t)blockIdx.x * (BLOCK / W) + threadIdx.x / W;
+    if (env >= p.B) return;
+    SEnv<EPL> v;
+    slice_load<W, EPL>(p, env, lane, v);
+    const int a = p.actions ? p.actions[env] : random_action(p, env, v.acc3, v.s.step);  // fused random policy
+    slice_step_body<W, EPL, TRACE, true>(p, env, lane, v, a, p.obs, p.reward, p.done);
+    if (lane == 0) slice_store_scalars<EPL>(p, env, v);
+}
+
+// envs/baselines.py (:6-35) on the slice's registers: argmin topology latency / argmax
+// zone cpu capacity / argmin endpoint cpu over feasible = mask[:-1] (masks are all True,
+// :808-821, so the endpoints e < A - 1), first index on ties; or the uniform random action.
+// Same values as k_policy / lb_policy.
+template <int W, int EPL>
+__device__ __forceinline__ int slice_policy(const Params& p, int64_t env, int lane, const SEnv<EPL>& v, int kind) {
+    if (kind == LB_POLICY_RANDOM) return random_action(p, env, v.acc3, v.s.step);
+    const int nf = p.A - 1;
+    if (nf <= 0) return p.A - 1;
+    double best = 0.0;
+    int bi = 1 << 30;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+        const int e = lane + k * W;
+        if (e >= nf) continue;
+        const int z = em_zone(v.em[k]);
+        double val;
+        if (kind == LB_POLICY_TOPOLOGY_GREEDY) val = (double)topo_val(v.topo, z, v.s.rz);
+        else if (kind == LB_POLICY_ZONE_CPU_GREEDY) val = -(double)zcap_val(v.zcap, z);
+        else val = p.cpu_lut[ed_m(v.ed[k]) * CPU_ROWS + em_c0(v.em[k])];
+        if (bi == (1 << 30) || val < best) { best = val; bi = e; }
+    }
+#pragma unroll
+    for (int m = W / 2; m >= 1; m >>= 1) {  // (value, index) minimum over the slice, lower index on ties
+        const double ob = __shfl_xor(best, m, W);
+        const int oi = __shfl_xor(bi, m, W);
+        const bool take = oi != (1 << 30) && (bi == (1 << 30) || ob < best || (ob == best && oi < bi));
+        best = take ? ob : best;
+        bi = take ? oi : bi;
+    }
+    return bi;
+}
+
+// lb_rollout: K steps per launch under an on-device policy, the env state held in
+// registers between steps; step k's obs / reward / done go to slot k of the caller's
+// buffers.  Bit for bit K x (lb_policy + lb_step) (tests/test_gpu_api.py).
+template <int W, int EPL>
+__global__ __launch_bounds__(BLOCK) void k_rollout_slice(Params p, int kind, int K, int32_t* act_out) {
+    const int lane = threadIdx.x % W;
+    const int64_t env = (int64_t)blockIdx.x * (BLOCK / W) + threadIdx.x / W;
+    if (env >= p.B) return;
+    SEnv<EPL> v;
+    slice_load<W, EPL>(p, env, lane, v);
+    const int64_t obs_slot = p.B * (int64_t)p.R * 8;
+    for (int k = 0; k < K; ++k) {
+        const int a = slice_policy<W, EPL>(p, env, lane, v, kind);
+        if (act_out && lane == 0) act_out[k * p.B + env] = a;
+        slice_step_body<W, EPL, false, false>(p, env, lane, v, a, p.obs ? p.obs + k * obs_slot : nullptr,
+                                               p.reward ? p.reward + k * p.B : nullptr,
+                                               p.done ? p.done + k * p.B : nullptr);
+    }
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+        const int e = lane + k * W;
+        if (e < p.E) p.edyn[eidx(p, env, e)] = v.ed[k];
+    }
     if (lane == 0) slice_store_scalars<EPL>(p, env, v);
 }
 

@@ -91,6 +91,7 @@ def lib():
     L.lb_reset.argtypes = [vp, cfgp, i64, vp, vp, trp, vp]
     L.lb_step.argtypes = [vp, cfgp, i64, vp, vp, vp, vp, vp, vp, trp, vp]
     L.lb_policy.argtypes = [vp, cfgp, i64, i32, vp, vp]
+    L.lb_rollout.argtypes = [vp, cfgp, i64, i32, i32, vp, vp, vp, vp, vp, vp, vp]
     L.lb_get_field.argtypes = [vp, cfgp, i64, i32, vp, vp]
     L.lb_get_stats.argtypes = [vp, cfgp, i64, vp, vp]
     L.lb_status.argtypes = [vp, cfgp, i64, vp, vp]
@@ -103,7 +104,7 @@ def lib():
     L.lb_ds_train_forward.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp]
     L.lb_ds_pack_backward.argtypes = [C.POINTER(LBDSWeightsC), vp, vp]
     L.lb_ds_train_backward.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp]
-    for f in ("lb_validate_config", "lb_state_bytes", "lb_init", "lb_reset", "lb_step", "lb_policy",
+    for f in ("lb_validate_config", "lb_state_bytes", "lb_init", "lb_reset", "lb_step", "lb_policy", "lb_rollout",
               "lb_get_field", "lb_get_stats", "lb_status", "lb_ds_pack", "lb_ds_forward",
               "lb_ds_train_forward", "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax",
               "lb_replay_add", "lb_ppo_head"):
@@ -126,6 +127,6 @@ def check(rc):
 
 
 EXPORTED_SYMBOLS = ("lb_abi_version", "lb_last_error", "lb_validate_config", "lb_state_bytes",
-                    "lb_init", "lb_reset", "lb_step", "lb_policy", "lb_get_field", "lb_get_stats",
+                    "lb_init", "lb_reset", "lb_step", "lb_policy", "lb_rollout", "lb_get_field", "lb_get_stats",
                     "lb_status", "lb_ds_pack", "lb_ds_forward", "lb_ds_train_forward",
                     "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax", "lb_replay_add", "lb_ppo_head")

@@ -406,6 +406,23 @@ class LBVecEnv:
             self._ptr(ep_stats_out if ep_stats_out is not None else self.ep_stats),
             C.byref(self._trace) if self.trace_mode else None, self._stream()))
 
+    def rollout(self, kind, steps, obs_out=None, reward_out=None, done_out=None, actions_out=None,
+                terminal_obs_out=None, ep_stats_out=None):
+        """`steps` vector steps under an on-device policy ("topo" / "zone_cpu" /
+        "endpoint_cpu" / "random") in one launch (lb_rollout): the same trajectory as
+        `steps` x (policy(kind), step_device(actions)).  Step k's outputs go to slot k of
+        obs_out (K, B, R, 8), reward_out (K, B), done_out (K, B) uint8, actions_out (K, B)
+        int32 (each None = not written)."""
+        if not self._reset_called:
+            raise TypeError("step() called before reset()")
+        if self.trace_mode:
+            raise RuntimeError("rollout() draws from Philox; trace mode steps one call at a time")
+        _native.check(self._L.lb_rollout(
+            self._ptr(self.state), C.byref(self._c), self.num_envs, _native.LB_POLICY[kind], int(steps),
+            self._ptr(obs_out), self._ptr(reward_out), self._ptr(done_out), self._ptr(actions_out),
+            self._ptr(terminal_obs_out if terminal_obs_out is not None else self.terminal_obs),
+            self._ptr(ep_stats_out if ep_stats_out is not None else self.ep_stats), self._stream()))
+
     def policy(self, kind, out=None):
         """Batched envs/baselines.py greedy policy or uniform random -> (B,) int32 device tensor."""
         out = out if out is not None else self.torch.empty(self.num_envs, dtype=self.torch.int32,

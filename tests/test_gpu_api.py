@@ -262,3 +262,63 @@ def test_vecmonitor_file_during_training(tmp_path):
     assert len(rows) == 64 * 4  # 2 updates x 20 steps / episode length 10
     rets = np.array([float(r["r"]) for r in rows])
     assert abs(rets.mean() - np.mean(algo.episode_returns)) < 1e-3 * max(1.0, abs(rets.mean()))
+
+
+@pytest.mark.parametrize("B,kw,geometry", [
+    (4096, {}, "auto"),                                                        # config 2 shape
+    (2000, dict(num_endpoints=6, num_nodes=48, num_zones=12, reward_function="multi"), "auto"),
+    (3000, dict(num_endpoints=64, reward_function="multi"), "auto"),
+    (40000, dict(num_endpoints=20, reward_function="fairness"), "auto"),       # 4-envs-per-wave slice
+    (40000, {}, "slice"),
+    (40000, dict(num_endpoints=6), "tpe"),                                     # K policy + step launches
+])
+@pytest.mark.parametrize("kind", ["random", "topo", "zone_cpu", "endpoint_cpu"])
+def test_rollout_equals_policy_plus_step(B, kw, geometry, kind):
+    """lb_rollout (K steps in one launch, the policy evaluated on the state in registers)
+    == K x (lb_policy + lb_step), bit for bit, across auto-resets."""
+    from lbk8s import LBVecEnv
+    K, L = 13, 5
+    a_env = LBVecEnv(B, seed=21, as_tensors=True, episode_length=L, geometry=geometry, **kw)
+    b_env = LBVecEnv(B, seed=21, as_tensors=True, episode_length=L, geometry=geometry, **kw)
+    a_env.reset()
+    b_env.reset()
+    R = a_env.cfg.obs_rows
+    obs = torch.empty((K, B, R, 8), device="cuda")
+    rew = torch.empty((K, B), device="cuda")
+    dn = torch.empty((K, B), dtype=torch.uint8, device="cuda")
+    act = torch.empty((K, B), dtype=torch.int32, device="cuda")
+    a_env.rollout(kind, K, obs_out=obs, reward_out=rew, done_out=dn, actions_out=act)
+    for k in range(K):
+        ak = b_env.policy(kind)
+        assert torch.equal(act[k], ak), k
+        b_env.step_device(ak)
+        assert torch.equal(obs[k], b_env.obs), k
+        assert torch.equal(rew[k], b_env.rewards), k
+        assert torch.equal(dn[k], b_env.dones), k
+    assert torch.equal(a_env.stats(), b_env.stats())
+    assert torch.equal(a_env.terminal_obs, b_env.terminal_obs)
+    for f in ("endpoint_latency", "endpoint_cpu_usage_percentage", "avg_load_served"):
+        assert torch.equal(a_env.field(f), b_env.field(f)), f
+    # the env goes on from where the rollout left it
+    a_env.step_device(act[0])
+    b_env.step_device(act[0])
+    assert torch.equal(a_env.obs, b_env.obs)
+    assert a_env.status() == 0
+
+
+def test_run_baselines_greedy_matches_oracle(oracle_mod):
+    """Config 1 driver (run_baselines.py): one launch per 100-step episode batch; every
+    episode's return and final accumulators equal the oracle's greedy episodes."""
+    from lbk8s.info import ST_RETURN
+    from lbk8s.run_baselines import CFG1, run_baselines
+    n = 512
+    for kind in ("topo", "zone_cpu", "endpoint_cpu"):
+        res = run_baselines(kind, n, seed=42)
+        orc = oracle_mod.OracleBatch(CFG1, n, trace=False, auto_reset=False, seed=42)
+        orc.init()
+        orc.reset()
+        for s in range(CFG1["episode_length"]):
+            _, r, _, _, _ = orc.step(orc.policy_greedy(kind))
+            np.testing.assert_array_equal(res["rewards"][s], r)
+        np.testing.assert_array_equal(res["returns"], orc.stats()[:, ST_RETURN])
+        assert (res["returns"] == 100).all()  # greedy never rejects (masks all True), naive +1
