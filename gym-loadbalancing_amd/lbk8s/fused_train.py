@@ -32,7 +32,9 @@ DSV = _native.LB_DSV
 
 
 def supported(actor_net, x) -> bool:
-    return fused.ENABLED and fused._geometry_ok(actor_net, x)
+    """The training kernels take R <= LB_DS_MAX_ELEMENTS (80); larger sets train through
+    the torch modules (with their GPU custom backward, deepsets._EquivariantFn)."""
+    return fused.ENABLED and fused._geometry_ok(actor_net, x) and x.shape[1] <= _native.LB_DS_MAX_ELEMENTS
 
 
 def _stream(dev):
