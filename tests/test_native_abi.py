@@ -113,3 +113,18 @@ def test_config_mirrors_reference_constructor_errors():
     assert c.observation_space().shape == (6, 8)
     assert c.action_space().n == 6
     assert LBConfig().observation_space().shape == (9, 8)
+
+
+def test_host_asan_ubsan_abi():
+    """The C ABI's host code under AddressSanitizer + UBSan (tests/asan/abi_asan.cpp):
+    validation, state-layout arithmetic, argument checks, error reporting, launch paths
+    without a GPU (device code unsanitized: GPU sanitizers are not available on this pool)."""
+    import shutil
+    import subprocess
+    if shutil.which("make") is None or not os.path.exists("/opt/rocm/bin/hipcc"):
+        pytest.skip("no hipcc / make")
+    r = subprocess.run(["make", "-s", "-C", os.path.join(REPO, "tests", "asan"), "run"], capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    assert "abi_asan: ok" in r.stdout
+    assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
