@@ -749,7 +749,7 @@ int lb_ds_train_backward(const float* bwd_frag, const float* obs, int64_t num_en
                          const float* save_actor, const float* save_critic, const float* dlogits, const float* dmean,
                          float* wgrad_out, float* workspace, float* setvec, void* stream) {
     static_assert(DSV_FLOATS == LB_DS_SETVEC_FLOATS, "per-set vector layout and header disagree");
-    static_assert(DSW_FLOATS == LB_DS_WGRAD_FLOATS && DSW_SLOTS * 2 * DSW_FLOATS == LB_DS_WORKSPACE_FLOATS,
+    static_assert(DSW_FLOATS == LB_DS_WGRAD_FLOATS && DSW_SLOTS * 2 * DSW_FLOATS <= LB_DS_WORKSPACE_FLOATS,
                   "weight-gradient layout and header disagree");
     if (!bwd_frag || !obs || !setvec || !wgrad_out || !workspace || num_envs < 1)
         return fail("bwd_frag/obs/setvec/wgrad_out/workspace NULL or num_envs < 1");
@@ -759,26 +759,12 @@ int lb_ds_train_backward(const float* bwd_frag, const float* obs, int64_t num_en
     if ((actor && !save_actor) || (critic && !save_critic)) return fail("a head's activation buffer is NULL");
     DSBwdParams p{obs, bwd_frag, save_actor, save_critic, dlogits, dmean, workspace, setvec,
                   num_envs, num_elements, actor, critic};
-    // fixed grid: one workspace slot per wave, so the reduction order never depends on B
+    // fixed grid: one workspace slot per block, so the reduction order never depends on B
     hipStream_t s = (hipStream_t)stream;
-    const int ts = (num_elements + 15) / 16;
-    for (int head = 0; head < 2; ++head) {
-        if (!(head == 0 ? actor : critic)) continue;
-#define LBK_BWD(TS)                                                                                          \
-    do {                                                                                                     \
-        if (head == 0) hipLaunchKernelGGL((k_ds_train_bwd<TS, 0>), dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);  \
-        else hipLaunchKernelGGL((k_ds_train_bwd<TS, 1>), dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);            \
-    } while (0)
-        switch (ts) {
-            case 1: LBK_BWD(1); break;
-            case 2: LBK_BWD(2); break;
-            case 3: LBK_BWD(3); break;
-            case 4: LBK_BWD(4); break;
-            default: LBK_BWD(5); break;
-        }
-#undef LBK_BWD
-        if (int r = check_launch()) return r;
-    }
+    if (actor) hipLaunchKernelGGL(k_ds_train_bwd<0>, dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);
+    if (int r = check_launch()) return r;
+    if (critic) hipLaunchKernelGGL(k_ds_train_bwd<1>, dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);
+    if (int r = check_launch()) return r;
     static_assert(DSW_SLOTS % (2 * DSR_GROUPS) == 0, "reduction stride");
     hipLaunchKernelGGL(k_ds_wgrad_reduce, dim3((2 * DSW_FLOATS + DSR_COLS - 1) / DSR_COLS), dim3(DSR_COLS * DSR_GROUPS),
                        0, s, workspace, wgrad_out, (int)actor, (int)critic);

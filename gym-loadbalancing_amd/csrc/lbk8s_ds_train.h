@@ -8,18 +8,22 @@
 //   * k_deepsets_fwd<TS, P, true> (lbk8s_deepsets.h) writes the logits, the critic's psi
 //     mean and the hidden activations h1, h2 (actor) / c1, c2 (critic) row-major.
 //   * torch evaluates rho, the PPO loss and its gradient w.r.t. logits and psi mean.
-//   * k_ds_train_bwd (here), one wave per set: back through every equivariant layer in
-//     registers — the set-wise max's argmax is recomputed from the saved activation, the
-//     activation derivative is taken from the activation itself (ReLU: y > 0; ELU: y > 0 ?
-//     1 : y + 1), the data gradient of each 64x64 layer is an f32 MFMA against the
-//     transposed Lambda.  The two big weight gradients of each head, dLambda2 = dz2^T h1
-//     (64x64) and dLambda1 = dz1^T obs (64x8), are accumulated over all the sets a wave
-//     visits by MFMA (contraction over rows: each 16-row tile is transposed through a
-//     per-wave LDS buffer) in accumulator registers, written once per wave into a slot of
-//     a workspace, and summed over slots by k_ds_wgrad_reduce: no per-row gradient ever
-//     reaches HBM.  Per-set vectors (set-wise max, gradient sums over the set, the
-//     last-layer products) give every Gamma gradient and the rank-1 last-layer gradients
-//     as small GEMMs over the sets.
+//   * k_ds_train_bwd (here), one wave per set, 8 waves per CU (2 per SIMD, so one wave's
+//     vector work runs beside the other's matrix work), the set streamed 16 rows at a time
+//     in two passes:
+//       pass 1 (h2, h1): every set-wise max and its FIRST argmax row (torch.max's index)
+//         in one sweep, the set sums the Gamma / Lambda3 gradients need, and the set sum
+//         of dz2 in closed form: sum_r dz2[r][o] = Lambda3[o] sum_r dl[r] elu'(h2[r][o])
+//         - g3 Gamma3[o] elu'(max_r h2[r][o]) (the critic: u, vv for Lambda3, Gamma3);
+//       pass 2, per 16-row tile: dz2 from h2; dLambda2 += dz2^T h1 (MFMA over rows: the
+//         tiles go through a per-wave LDS transpose); the data gradient dz1 = (dz2
+//         Lambda2 - [r == argmax] Gamma2^T sum dz2) act'(h1) (f32 MFMA); dLambda1 += dz1^T obs.
+//     The weight-gradient accumulators stay in registers across all the sets a wave
+//     visits; at the end the block sums its 8 waves in LDS in a fixed order and writes one
+//     slot, and k_ds_wgrad_reduce sums the slots in a fixed order: no per-row gradient
+//     reaches HBM, and the result does not depend on timing.  Per-set vectors (set-wise
+//     max, gradient sums over the set, the last-layer products) give every Gamma gradient
+//     and the rank-1 last-layer gradients as small GEMMs over the sets.
 // Layout conventions (fragment order, accumulator layout) are those of lbk8s_deepsets.h:
 // lane l holds set element (l & 15) of each 16-row tile, and at k-step k the features
 // 16(k >> 2) + 4(l >> 4) + (k & 3).
@@ -51,11 +55,12 @@ enum : int {
     DSV_FLOATS = 648,
 };
 
-constexpr int DSB_BLOCK = 256;                       // 4 waves, 1 per SIMD: 512 registers per lane
+constexpr int DSB_BLOCK = 512;                       // 8 waves: 2 per SIMD, one block per CU
 constexpr int DSW_FLOATS = 4608;                     // per head: dLambda2 [64][64], dLambda1 [64][8]
-constexpr int DSW_SLOTS = 1024;                      // one per wave of the fixed grid
-constexpr int DSW_GRID = DSW_SLOTS / (DSB_BLOCK / 64);
-constexpr int DST_STRIDE = 80;                       // LDS transpose row stride (floats): 16 banks per row group
+constexpr int DSW_GRID = 256;                        // fixed grid (any B): one block per CU
+constexpr int DSW_SLOTS = DSW_GRID;                  // one partial-sum slot per block
+constexpr int DST_STRIDE = 80;                       // LDS transpose row stride (floats)
+constexpr int DSB_LDS_W = 16384;                     // head weights in LDS (the critic's four 64x64)
 
 struct DSBwdParams {
     const float* obs;          // [B][R][8]
@@ -64,33 +69,49 @@ struct DSBwdParams {
     const float* save_critic;  // [2][B][R][64] c1, c2
     const float* dlogits;      // [B][R]
     const float* dmean;        // [B][64]
-    float* wpart;              // [DSW_SLOTS][2][DSW_FLOATS] per-wave weight-gradient partials
+    float* wpart;              // [DSW_SLOTS][2][DSW_FLOATS] per-block weight-gradient partials
     float* setvec;             // [B][DSV_FLOATS]
     int64_t B;
     int R;
     int actor, critic;
 };
 
-template <int TS>
-__device__ __forceinline__ void load_rows(const float* plane, float (&h)[TS][16], int64_t env, int R, int col,
-                                          int grp) {
+// element (row, feature f) of a staged 16-row tile: rows 80 floats apart, the feature index
+// XOR-swizzled by 4 (row & 7) (groups of 4 features stay contiguous), so the row-major
+// float4 stores of 8 consecutive rows and the transposed reads (4 rows x 16 features per
+// 32 lanes) are bank-conflict free.  TBOff holds that index for each access pattern in
+// closed form: a few lane offsets, the rest compile-time constants.
+struct TBOff {
+    int rd;        // transposed reads, row 4c + grp, feature col + 16m:  rd + 320c + 16 (m ^ (c & 1))
+    int we, wo;    // row-major float4 stores, row col, features 16nt + 4grp:  (nt even ? we : wo) + 16nt
+    int w80, w81;  // observation stores, row col, feature 4kk + grp (kk = 0, 1)
+    int r8;        // observation reads, row 4c + grp, feature col & 7:  r8 + 320c + 16 (c & 1)
+};
+__device__ __forceinline__ TBOff tb_offsets(int col, int grp) {
+    static_assert(DST_STRIDE == 80, "closed forms assume 80-float rows");
+    TBOff o;
+    const int b = (col >> 2) & 1, base0 = col * DST_STRIDE + 4 * (grp ^ (col & 3));
+    o.rd = grp * DST_STRIDE + (col ^ (4 * grp));
+    o.we = base0 + 16 * b;
+    o.wo = base0 - 16 * b;
+    o.w80 = col * DST_STRIDE + grp + 4 * (col & 7);
+    o.w81 = col * DST_STRIDE + grp + 4 * (1 ^ (col & 7));
+    o.r8 = grp * DST_STRIDE + ((col & 7) ^ (4 * grp));
+    return o;
+}
+
+// one 16-row tile of a [B][R][64] plane in fragment layout (lane: row 16t + col, features
+// 16nt + 4grp + i); rows past R read row R - 1 (in bounds, no branch) and are zeroed
+__device__ __forceinline__ void load_tile(const float* plane, float (&h)[16], int64_t env, int R, int row, int grp) {
+    const bool ok = row < R;
+    const float* q = plane + (env * (int64_t)R + (ok ? row : R - 1)) * 64 + 4 * grp;
 #pragma unroll
-    for (int t = 0; t < TS; ++t) {
-        const int row = 16 * t + col;
-        if (row < R) {
-            const float* q = plane + (env * (int64_t)R + row) * 64 + 4 * grp;
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt) {
-                const float4 v = *reinterpret_cast<const float4*>(q + 16 * nt);
-                h[t][4 * nt] = v.x;
-                h[t][4 * nt + 1] = v.y;
-                h[t][4 * nt + 2] = v.z;
-                h[t][4 * nt + 3] = v.w;
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) h[t][k] = 0.f;
-        }
+    for (int nt = 0; nt < 4; ++nt) {
+        const float4 v = *reinterpret_cast<const float4*>(q + 16 * nt);
+        h[4 * nt] = ok ? v.x : 0.f;
+        h[4 * nt + 1] = ok ? v.y : 0.f;
+        h[4 * nt + 2] = ok ? v.z : 0.f;
+        h[4 * nt + 3] = ok ? v.w : 0.f;
     }
 }
 
@@ -105,105 +126,49 @@ __device__ __forceinline__ void store_vec(float* dst, const float (&v)[16], int 
 // argmax rows (< 80) of 16 features, one byte each: id[k >> 2] byte (k & 3)
 __device__ __forceinline__ int id_of(const int (&id)[4], int k) { return (id[k >> 2] >> (8 * (k & 3))) & 0xff; }
 
-// per feature: max over the set's valid rows and the FIRST row attaining it (torch.max's
-// index, where the reference's autograd sends the pooled gradient)
-template <int TS>
-__device__ __forceinline__ void set_max_idx(const float (&h)[TS][16], float (&mx)[16], int (&id)[4], int col, int R) {
-    float m[16], c[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        float v = -INFINITY;
-#pragma unroll
-        for (int t = 0; t < TS; ++t)
-            if (16 * t + col < R) v = max2(v, h[t][k]);
-        m[k] = v;
-    }
-    row_reduce<true>(m);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        float v = -1e9f;  // max of -row == min row
-#pragma unroll
-        for (int t = 0; t < TS; ++t) {
-            const int row = 16 * t + col;
-            if (row < R && h[t][k] == m[k]) v = max2(v, -(float)row);
-        }
-        c[k] = v;
-    }
-    row_reduce<true>(c);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) mx[k] = m[k];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        id[q] = (int)(-c[4 * q]) | ((int)(-c[4 * q + 1]) << 8) | ((int)(-c[4 * q + 2]) << 16) | ((int)(-c[4 * q + 3]) << 24);
-}
-
-// sum over the set (rows past R hold 0)
-template <int TS>
-__device__ __forceinline__ void set_sum(const float (&h)[TS][16], float (&s)[16]) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        float v = 0.f;
-#pragma unroll
-        for (int t = 0; t < TS; ++t) v += h[t][k];
-        s[k] = v;
-    }
-    row_reduce<false>(s);
-}
-
 // d act / d z from the activation's output: ReLU (ACT 1) y > 0; ELU (ACT 2) y > 0 ? 1 : y + 1
 template <int ACT>
 __device__ __forceinline__ float dact(float y) {
     return ACT == 1 ? (y > 0.f ? 1.f : 0.f) : (y > 0.f ? 1.f : y + 1.f);
 }
 
-// Back through a 64 -> 64 equivariant layer z = Lambda h - Gamma max_set(h), h = act(z_prev):
-// g = dz (this layer), gs = sum_r dz; h (in: the layer input, out: dz of the layer below)
-//   dh[r][i] = sum_o Lambda[o][i] dz[r][o] - [r == argmax_i] sum_o Gamma[o][i] gs[o]
-//   dz_prev  = dh * act'(h)
-template <int TS, int ACT>
-__device__ __forceinline__ void eq_back64(const float* LT, const float* GT, const float (&g)[TS][16],
-                                          const float (&gs)[16], float (&h)[TS][16], const int (&id)[4], int lane,
-                                          int col, int R) {
+// per-lane running (max, first row) of a pass-1 sweep -> the set's max and FIRST argmax row
+// (torch.max's index) per feature: the max over the 16 lanes of the row group, then the
+// smallest row among the lanes that hold it
+__device__ __forceinline__ void finish_argmax(float (&m)[16], const float (&r)[16], int (&id)[4]) {
+    float M[16], c[16];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-        dsf4 v = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < 16; ++k) M[k] = m[k];
+    row_reduce<true>(M);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) v = mfma4(GT[(nt * 16 + k) * 64 + lane], gs[k], v);
+    for (int k = 0; k < 16; ++k) c[k] = m[k] == M[k] ? -r[k] : -1e9f;
+    row_reduce<true>(c);
 #pragma unroll
-        for (int t = 0; t < TS; ++t) {
-            dsf4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < 16; ++k) m[k] = M[k];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) acc = mfma4(LT[(nt * 16 + k) * 64 + lane], g[t][k], acc);
-            const int row = 16 * t + col;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int kk = 4 * nt + i;
-                const float x = acc[i] - (row == id_of(id, kk) ? v[i] : 0.f);
-                h[t][kk] = row < R ? x * dact<ACT>(h[t][kk]) : 0.f;
-            }
-        }
-    }
+    for (int q = 0; q < 4; ++q)
+        id[q] = (int)(-c[4 * q]) | ((int)(-c[4 * q + 1]) << 8) | ((int)(-c[4 * q + 2]) << 16) | ((int)(-c[4 * q + 3]) << 24);
 }
 
-// stage one 16-row tile (this lane: row col, features 16nt + 4grp + i) row-major in LDS
-__device__ __forceinline__ void stage_tile(float* buf, const float (&v)[16], int col, int grp) {
-    float* q = buf + col * DST_STRIDE + 4 * grp;
+// stage one 16-row tile (this lane: row col, features 16nt + 4grp + i) in LDS
+__device__ __forceinline__ void stage_tile(float* buf, const float (&v)[16], const TBOff& o) {
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
-        *reinterpret_cast<float4*>(q + 16 * nt) = make_float4(v[4 * nt], v[4 * nt + 1], v[4 * nt + 2], v[4 * nt + 3]);
+        *reinterpret_cast<float4*>(buf + (nt % 2 == 0 ? o.we : o.wo) + 16 * nt) =
+            make_float4(v[4 * nt], v[4 * nt + 1], v[4 * nt + 2], v[4 * nt + 3]);
 }
 
 // acc[mt][nt] += dz^T h over one staged 16-row tile: MFMA k-step c contracts rows
 // 4c..4c+3; A[m][kk] = dz[4c + kk][16mt + m], B[kk][n] = h[4c + kk][16nt + n]
-__device__ __forceinline__ void wgrad64(const float* la, const float* lb, dsf4 (&acc)[4][4], int col, int grp) {
+__device__ __forceinline__ void wgrad64(const float* la, const float* lb, dsf4 (&acc)[4][4], const TBOff& o) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         float av[4], bv[4];
-        const int r = (4 * c + grp) * DST_STRIDE + col;
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
-            av[m] = la[r + 16 * m];
-            bv[m] = lb[r + 16 * m];
+            const int i = o.rd + 320 * c + 16 * (m ^ (c & 1));
+            av[m] = la[i];
+            bv[m] = lb[i];
         }
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
@@ -212,88 +177,46 @@ __device__ __forceinline__ void wgrad64(const float* la, const float* lb, dsf4 (
     }
 }
 
-// acc[mt] += dz^T obs over one staged tile: the tile's observation rows (h0: this lane holds
-// features 4kk + grp of row col) are staged next to it, B columns 8..15 read as zero
-template <int TS>
-__device__ __forceinline__ void wgrad8(const float* la, float* lb, const float (&h0)[TS][2], int t, dsf4 (&acc)[4],
-                                       int col, int grp) {
-    lb[col * DST_STRIDE + grp] = h0[t][0];
-    lb[col * DST_STRIDE + 4 + grp] = h0[t][1];
+// acc[mt] += dz^T obs over one staged tile (dz1 in la): the tile's observation rows (this
+// lane: features grp and 4 + grp of row col) are staged in lb, B columns 8..15 read as zero
+__device__ __forceinline__ void wgrad8(const float* la, float* lb, const float (&x0)[2], dsf4 (&acc)[4], int col,
+                                       const TBOff& o) {
+    lb[o.w80] = x0[0];
+    lb[o.w81] = x0[1];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        const int r = (4 * c + grp) * DST_STRIDE + col;
-        const float xv = col < 8 ? lb[r] : 0.f;
+        const float x = lb[o.r8 + 320 * c + 16 * (c & 1)];
+        const float xv = col < 8 ? x : 0.f;
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) acc[mt] = mfma4(la[r + 16 * mt], xv, acc[mt]);
+        for (int mt = 0; mt < 4; ++mt) acc[mt] = mfma4(la[o.rd + 320 * c + 16 * (mt ^ (c & 1))], xv, acc[mt]);
     }
 }
 
-// a set's observation in fragment layout: h0[t][kk] = feature 4kk + grp of row 16t + col
-template <int TS>
-__device__ __forceinline__ void load_obs(const float* obs, int64_t env, int R, int col, int grp, float (&h0)[TS][2]) {
-    const float* x = obs + env * (int64_t)R * 8;
-#pragma unroll
-    for (int t = 0; t < TS; ++t) {
-        const int row = 16 * t + col;
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) h0[t][kk] = row < R ? x[row * 8 + 4 * kk + grp] : 0.f;
-    }
-}
-
-// the head's upstream gradient for one set: actor dlogits rows (dl), critic dmean (gm, k layout)
-template <int TS, int HEAD>
-__device__ __forceinline__ void load_upstream(const DSBwdParams& p, int64_t env, int col, int grp, float (&dl)[TS],
-                                              float (&gm)[16]) {
-    if (HEAD == 0) {
-#pragma unroll
-        for (int t = 0; t < TS; ++t) {
-            const int row = 16 * t + col;
-            dl[t] = row < p.R ? p.dlogits[env * p.R + row] : 0.f;
-        }
-    } else {
-        const float* q = p.dmean + env * 64 + 4 * grp;
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-            const float4 v = *reinterpret_cast<const float4*>(q + 16 * nt);
-            gm[4 * nt] = v.x;
-            gm[4 * nt + 1] = v.y;
-            gm[4 * nt + 2] = v.z;
-            gm[4 * nt + 3] = v.w;
-        }
-    }
-}
-
-__device__ __forceinline__ void wpart_store(float* wp, const dsf4 (&a2)[4][4], const dsf4 (&a1)[4], int col, int grp) {
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int o = 16 * mt + 4 * grp + i;
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt) wp[o * 64 + 16 * nt + col] = a2[mt][nt][i];
-            if (col < 8) wp[4096 + o * 8 + col] = a1[mt][i];
-        }
-}
-
-// One launch per head (HEAD 0 actor, 1 critic): a head's 80 accumulator registers, its two
-// activation tiles and the set-wise bookkeeping fit the 512 registers of a wave.  With one
-// wave per SIMD nothing else hides memory latency, so the loop is software-pipelined: the
-// next set's layer-2 input is loaded as soon as the layer-2 tile is dead (after the data
-// gradient), its layer-1 input and observation once the dLambda1 tiles are done.
-template <int TS, int HEAD>
+// One launch per head (HEAD 0 actor, 1 critic).
+template <int HEAD>
 __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
-    __shared__ __attribute__((aligned(16))) float W[DSB_FLOATS];
+    constexpr int ACT1 = HEAD == 0 ? 1 : 2;  // activation after layer 1: ReLU (actor) / ELU (critic)
+    __shared__ __attribute__((aligned(16))) float W[DSB_LDS_W];
     __shared__ __attribute__((aligned(16))) float TB[DSB_BLOCK / 64][2][16 * DST_STRIDE];
-    for (int i = threadIdx.x * 4; i < DSB_FLOATS; i += DSB_BLOCK * 4)
-        *reinterpret_cast<float4*>(W + i) = *reinterpret_cast<const float4*>(p.wb + i);
+    // the head's weights: [0, 8192) Lambda2^T, Gamma2^T (fragment order); the actor's
+    // Lambda3 / Gamma3 rows at 8192 / 8256, the critic's Lambda3^T / Gamma3^T at 8192 / 12288
+    {
+        const int n = HEAD == 0 ? 8192 : 16384;
+        const float* src = p.wb + (HEAD == 0 ? DSB_A2LT : DSB_C2LT);
+        for (int i = threadIdx.x * 4; i < n; i += DSB_BLOCK * 4)
+            *reinterpret_cast<float4*>(W + i) = *reinterpret_cast<const float4*>(src + i);
+        if (HEAD == 0)
+            for (int i = threadIdx.x; i < 128; i += DSB_BLOCK) W[8192 + i] = p.wb[DSB_A3L + i];
+    }
     __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const int64_t wave = (int64_t)blockIdx.x * (DSB_BLOCK / 64) + (threadIdx.x >> 6);
+    const float* LT = W;  // (Gamma2^T at W + 4096)
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t nwaves = (int64_t)gridDim.x * (DSB_BLOCK / 64);
-    float* la = TB[threadIdx.x >> 6][0];
-    float* lb = TB[threadIdx.x >> 6][1];
-    const int R = p.R;
+    float* la = TB[wv][0];
+    float* lb = TB[wv][1];
+    const int R = p.R, ntl = (R + 15) / 16;
     const int col = lane & 15, grp = lane >> 4;
+    const TBOff tbo = tb_offsets(col, grp);
     const int64_t plane = p.B * (int64_t)R * 64;
     const float* in1 = HEAD == 0 ? p.save_actor : p.save_critic;  // h1 / c1
     const float* in2 = in1 + plane;                                 // h2 / c2
@@ -305,128 +228,200 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
         for (int nt = 0; nt < 4; ++nt) w2[mt][nt] = dsf4{0.f, 0.f, 0.f, 0.f};
         w1[mt] = dsf4{0.f, 0.f, 0.f, 0.f};
     }
-    float a[TS][16], h[TS][16], h0[TS][2], dl[TS], gm[16];
-    int64_t env = wave;
-    if (env < p.B) {
-        load_rows<TS>(in2, a, env, R, col, grp);
-        load_upstream<TS, HEAD>(p, env, col, grp, dl, gm);
-        load_rows<TS>(in1, h, env, R, col, grp);
-        load_obs<TS>(p.obs, env, R, col, grp, h0);
-    }
-    for (; env < p.B; env += nwaves) {
-        const int64_t nxt = env + nwaves;
+    for (int64_t env = (int64_t)blockIdx.x * (DSB_BLOCK / 64) + wv; env < p.B; env += nwaves) {
         float* sv = p.setvec + env * DSV_FLOATS;
-        float mx[16], gs[16];
-        int id[4];
-        if (HEAD == 0) {
-            set_max_idx<TS>(a, mx, id, col, R);
-            store_vec(sv + DSV_MAX2A, mx, col, grp);
-            // Lambda3 product and the set sum of dlogits, in one row reduction
-            float red[20];
+        // weights re-read from LDS per set (an opaque offset: no loop-invariant hoisting)
+        uint32_t wso = 0;
+        asm volatile("" : "+s"(wso));
+        const float* Ws = W + wso;
+        // ---- pass 1: set-wise maxima + first argmax rows, set sums
+        float mx2[16], r2[16], mx1[16], r1[16], S[16], G[16], g3 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            mx2[k] = mx1[k] = -INFINITY;
+            r2[k] = r1[k] = 0.f;
+            S[k] = G[k] = 0.f;
+        }
+        for (int t = 0; t < ntl; ++t) {
+            const int row = 16 * t + col;
+            const bool ok = row < R;
+            const float fr = (float)row;
+            float a[16], h[16];
+            load_tile(in2, a, env, R, row, grp);
+            load_tile(in1, h, env, R, row, grp);
+            float w = ok ? 1.f : 0.f;  // actor: dlogit of the row (0 past R); critic: row validity
+            if (HEAD == 0) {
+                const float d = p.dlogits[env * R + (ok ? row : R - 1)];
+                w = ok ? d : 0.f;
+                g3 += w;
+            }
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
-                float v = 0.f;
-#pragma unroll
-                for (int t = 0; t < TS; ++t) v += dl[t] * a[t][k];
-                red[k] = v;
+                const bool u2 = ok && a[k] > mx2[k];  // strict: rows ascend, the first maximum stays
+                mx2[k] = u2 ? a[k] : mx2[k];
+                r2[k] = u2 ? fr : r2[k];
+                S[k] += w * dact<2>(a[k]);
+                G[k] += HEAD == 0 ? w * a[k] : a[k];  // actor: sum dl h2 (Lambda3); critic: sum c2
+                const bool u1 = ok && h[k] > mx1[k];
+                mx1[k] = u1 ? h[k] : mx1[k];
+                r1[k] = u1 ? fr : r1[k];
             }
-            {
-                float v = 0.f;
-#pragma unroll
-                for (int t = 0; t < TS; ++t) v += dl[t];
-                red[16] = v;
-                red[17] = red[18] = red[19] = 0.f;
-            }
-            row_reduce<false>(red);
-            {
-                float ga[16];
-#pragma unroll
-                for (int k = 0; k < 16; ++k) ga[k] = red[k];
-                store_vec(sv + DSV_GA3, ga, col, grp);
-            }
-            const float g3 = red[16];
-            // dz2 = (dlogit Lambda3 - [r == argmax] g3 Gamma3) * elu'(h2)
+        }
+        int id2[4], id1[4];
+        finish_argmax(mx2, r2, id2);
+        finish_argmax(mx1, r1, id1);
+        row_reduce<false>(S);
+        row_reduce<false>(G);
+        store_vec(sv + (HEAD == 0 ? DSV_MAX2A : DSV_MAX2C), mx2, col, grp);
+        store_vec(sv + (HEAD == 0 ? DSV_GA3 : DSV_CS2), G, col, grp);
+        store_vec(sv + (HEAD == 0 ? DSV_MAX1A : DSV_MAX1C), mx1, col, grp);
+        // per feature o, dz2[r][o] = (c1[o] - [r == argmax] c2[o]) elu'(h2[r][o]) with
+        // actor c1 = dl[r] Lambda3[o] (row-dependent through dl), c2 = g3 Gamma3[o];
+        // critic c1 = u[o] = (Lambda3^T dmean)[o] / R, c2 = vv[o] = (Gamma3^T dmean)[o]
+        float c1[16], c2[16];
+        if (HEAD == 0) {
+            float gv[4] = {g3, 0.f, 0.f, 0.f};
+            row_reduce<false>(gv);
+            g3 = gv[0];
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 const int f = 16 * (k >> 2) + 4 * grp + (k & 3);
-                const float l3 = W[DSB_A3L + f], gg = g3 * W[DSB_A3G + f];
-#pragma unroll
-                for (int t = 0; t < TS; ++t) {
-                    const int row = 16 * t + col;
-                    const float x = dl[t] * l3 - (row == id_of(id, k) ? gg : 0.f);
-                    a[t][k] = row < R ? x * dact<2>(a[t][k]) : 0.f;
-                }
+                c1[k] = Ws[8192 + f];
+                c2[k] = g3 * Ws[8256 + f];
             }
         } else {
-            // d psi[r] = dmean / R on every row: u = Lambda3^T dmean / R (row-independent),
-            // vv = Gamma3^T (sum_r d psi[r]) = Gamma3^T dmean
-            float u[16], vv[16];
+            float gm[16];
+            const float* q = p.dmean + env * 64 + 4 * grp;
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                const float4 v = *reinterpret_cast<const float4*>(q + 16 * nt);
+                gm[4 * nt] = v.x;
+                gm[4 * nt + 1] = v.y;
+                gm[4 * nt + 2] = v.z;
+                gm[4 * nt + 3] = v.w;
+            }
             const float invR = 1.0f / (float)R;
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt) {
                 dsf4 uu = {0.f, 0.f, 0.f, 0.f}, w = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int k = 0; k < 16; ++k) {
-                    uu = mfma4(W[DSB_C3LT + (nt * 16 + k) * 64 + lane], gm[k] * invR, uu);
-                    w = mfma4(W[DSB_C3GT + (nt * 16 + k) * 64 + lane], gm[k], w);
+                    uu = mfma4(Ws[8192 + (nt * 16 + k) * 64 + lane], gm[k] * invR, uu);
+                    w = mfma4(Ws[12288 + (nt * 16 + k) * 64 + lane], gm[k], w);
                 }
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    u[4 * nt + i] = uu[i];
-                    vv[4 * nt + i] = w[i];
+                    c1[4 * nt + i] = uu[i];
+                    c2[4 * nt + i] = w[i];
                 }
             }
-            set_max_idx<TS>(a, mx, id, col, R);
-            store_vec(sv + DSV_MAX2C, mx, col, grp);
-            set_sum<TS>(a, gs);
-            store_vec(sv + DSV_CS2, gs, col, grp);
-#pragma unroll
-            for (int k = 0; k < 16; ++k)
-#pragma unroll
-                for (int t = 0; t < TS; ++t) {
-                    const int row = 16 * t + col;
-                    const float x = u[k] - (row == id_of(id, k) ? vv[k] : 0.f);
-                    a[t][k] = row < R ? x * dact<2>(a[t][k]) : 0.f;
-                }
         }
-        set_sum<TS>(a, gs);
+        // sum over the set of dz2, in closed form from pass 1's sums (S = sum of dl elu'(h2)
+        // for the actor, of elu'(c2) over the set's rows for the critic)
+        float gs[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) gs[k] = c1[k] * S[k] - c2[k] * dact<2>(mx2[k]);
         store_vec(sv + (HEAD == 0 ? DSV_GS2A : DSV_GS2C), gs, col, grp);
-        set_max_idx<TS>(h, mx, id, col, R);
-        store_vec(sv + (HEAD == 0 ? DSV_MAX1A : DSV_MAX1C), mx, col, grp);
+        // v = Gamma2^T (sum dz2): the pooled part of the layer-1 data gradient
+        float v[16];
 #pragma unroll
-        for (int t = 0; t < TS; ++t) {
-            stage_tile(la, a[t], col, grp);
-            stage_tile(lb, h[t], col, grp);
-            wgrad64(la, lb, w2, col, grp);
-        }
-        if (HEAD == 0) eq_back64<TS, 1>(W + DSB_A2LT, W + DSB_A2GT, a, gs, h, id, lane, col, R);
-        else eq_back64<TS, 2>(W + DSB_C2LT, W + DSB_C2GT, a, gs, h, id, lane, col, R);
-        if (nxt < p.B) {  // layer-2 tile and upstream gradient are dead: prefetch the next set's
-            load_rows<TS>(in2, a, nxt, R, col, grp);
-            load_upstream<TS, HEAD>(p, nxt, col, grp, dl, gm);
-        }
-        set_sum<TS>(h, gs);
-        store_vec(sv + (HEAD == 0 ? DSV_GS1A : DSV_GS1C), gs, col, grp);
+        for (int nt = 0; nt < 4; ++nt) {
+            dsf4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int t = 0; t < TS; ++t) {
-            stage_tile(la, h[t], col, grp);
-            wgrad8<TS>(la, lb, h0, t, w1, col, grp);
+            for (int k = 0; k < 16; ++k) acc = mfma4(Ws[4096 + (nt * 16 + k) * 64 + lane], gs[k], acc);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[4 * nt + i] = acc[i];
         }
+        // ---- pass 2, per tile: dz2, dLambda2 += dz2^T h1, dz1, dLambda1 += dz1^T obs
+        float gs1[16], m0[2] = {-INFINITY, -INFINITY};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) gs1[k] = 0.f;
+        for (int t = 0; t < ntl; ++t) {
+            // Lambda2^T re-read from LDS per tile: an opaque offset keeps the compiler from
+            // hoisting its 64 loop-invariant fragments into registers (which spilled)
+            uint32_t wo = 0;
+            asm volatile("" : "+s"(wo));
+            const float* LTt = LT + wo;
+            const int row = 16 * t + col;
+            const bool ok = row < R;
+            float a[16], h[16], x0[2];
+            load_tile(in2, a, env, R, row, grp);
+            load_tile(in1, h, env, R, row, grp);
+            {
+                const float* x = p.obs + (env * (int64_t)R + (ok ? row : R - 1)) * 8;
+                x0[0] = ok ? x[grp] : 0.f;
+                x0[1] = ok ? x[4 + grp] : 0.f;
+            }
+            float d = 0.f;
+            if (HEAD == 0) {
+                const float dv = p.dlogits[env * R + (ok ? row : R - 1)];
+                d = ok ? dv : 0.f;
+            }
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const float x = (HEAD == 0 ? d * c1[k] : c1[k]) - (row == id_of(id2, k) ? c2[k] : 0.f);
+                a[k] = ok ? x * dact<2>(a[k]) : 0.f;
+            }
+            stage_tile(la, a, tbo);
+            stage_tile(lb, h, tbo);
+            wgrad64(la, lb, w2, tbo);
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                dsf4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int k = 0; k < 16; ++k) acc = mfma4(LTt[(nt * 16 + k) * 64 + lane], a[k], acc);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int kk = 4 * nt + i;
+                    const float x = acc[i] - (row == id_of(id1, kk) ? v[kk] : 0.f);
+                    h[kk] = ok ? x * dact<ACT1>(h[kk]) : 0.f;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 16; ++k) gs1[k] += h[k];
+            if (do_max0 && ok) {
+                m0[0] = max2(m0[0], x0[0]);
+                m0[1] = max2(m0[1], x0[1]);
+            }
+            stage_tile(la, h, tbo);
+            wgrad8(la, lb, x0, w1, col, tbo);
+        }
+        row_reduce<false>(gs1);
+        store_vec(sv + (HEAD == 0 ? DSV_GS1A : DSV_GS1C), gs1, col, grp);
         if (do_max0) {
-            float m0[2];
-            set_max_batched<TS, 1, 2>(h0, m0, col, R);
+            row_reduce<true>(m0);
             if (col == 0) {
                 sv[DSV_MAX0 + grp] = m0[0];
                 sv[DSV_MAX0 + 4 + grp] = m0[1];
             }
         }
-        if (nxt < p.B) {
-            load_rows<TS>(in1, h, nxt, R, col, grp);
-            load_obs<TS>(p.obs, nxt, R, col, grp, h0);
-        }
     }
-    // every wave of the fixed grid owns one slot (zeros if it saw no set)
-    wpart_store(p.wpart + wave * (2 * DSW_FLOATS) + HEAD * DSW_FLOATS, w2, w1, col, grp);
+    // the block's 8 waves summed in LDS in a fixed order, one slot per block
+    __syncthreads();
+    float* red = &TB[0][0][0];
+    static_assert(sizeof(TB) / sizeof(float) >= DSW_FLOATS, "reduction buffer");
+    for (int w = 0; w < DSB_BLOCK / 64; ++w) {
+        if (wv == w) {
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int o = 16 * mt + 4 * grp + i;
+#pragma unroll
+                    for (int nt = 0; nt < 4; ++nt) {
+                        float& r = red[o * 64 + 16 * nt + col];
+                        r = w == 0 ? w2[mt][nt][i] : r + w2[mt][nt][i];
+                    }
+                    if (col < 8) {
+                        float& r = red[4096 + o * 8 + col];
+                        r = w == 0 ? w1[mt][i] : r + w1[mt][i];
+                    }
+                }
+        }
+        __syncthreads();
+    }
+    float* slot = p.wpart + (int64_t)blockIdx.x * (2 * DSW_FLOATS) + HEAD * DSW_FLOATS;
+    for (int i = threadIdx.x; i < DSW_FLOATS; i += DSB_BLOCK) slot[i] = red[i];
 }
 
 // sum of the per-wave partials: out[j] = sum_s wpart[s][j], j < 2 * DSW_FLOATS; zeros for
