@@ -256,7 +256,11 @@ def main(argv=None):
         with open(args.pmc_json) as f:
             pmc = json.load(f)
         if pmc.get("config") == args.config and pmc.get("envs") == B:
+            # one bench step = the step kernel + the deferred-reset kernel (both inside the
+            # event window that kernel_ms comes from)
             traffic = pmc.get("hbm_bytes_per_launch")
+            if traffic is not None and pmc.get("reset_kernel"):
+                traffic += pmc["reset_kernel"]["hbm_bytes_per_launch"]
     except (OSError, ValueError):
         pass
     line = {
@@ -273,7 +277,8 @@ def main(argv=None):
                    "parallelism": f"env-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_step_tpe (lb_step)" if env.cfg.num_endpoints <= 8 else "k_step_slice (lb_step)",
+                     "kernel": ("k_step_tpe + k_reset_listed (lb_step)" if env.cfg.num_endpoints <= 8
+                                else "k_step_slice (lb_step)"),
                      "kernel_ms": kernel_ms, "bytes_per_env_step": b_alg, "envs_per_launch": B},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
-"""Workload for the rocprofv3 PMC passes: 10 lb_step launches at 2^20 default envs (obs ring
-of 16), then 3 torch copies of 1 GiB (known bytes: calibrates FETCH_SIZE / WRITE_SIZE)."""
+"""Workload for the rocprofv3 PMC passes: bench.py's timed step (2^20 default envs, the
+env's random policy drawn in the kernel, obs / reward / done ring of 16, episodes staggered
+so 1/episode_length of the envs end and auto-reset every step), 16 launches after the
+stagger setup, then 3 torch copies of 1 GiB (known bytes: calibrates FETCH_SIZE /
+WRITE_SIZE)."""
 import os
 import sys
 
@@ -19,10 +22,17 @@ def main():
     env = LBVecEnv(B, seed=0, as_tensors=True, **CONFIGS[cfg])
     R, T = env.cfg.obs_rows, 16
     ring = torch.empty((T, B, R, 8), dtype=torch.float32, device="cuda")
-    acts = torch.randint(0, env.action_space.n, (16, B), dtype=torch.int32, device="cuda")
+    rew = torch.empty((T, B), dtype=torch.float32, device="cuda")
+    done = torch.empty((T, B), dtype=torch.uint8, device="cuda")
+    L = env.cfg.episode_length
     env.reset()
-    for i in range(15):
-        env.step_device(acts[i], obs_out=ring[i % T])
+    gid = torch.arange(B, device="cuda")
+    for r in range(1, L):  # bench.py's stagger
+        env.step_device(None, obs_out=ring[0], reward_out=rew[0], done_out=done[0])
+        env.reset_masked((gid % L) == r)
+    torch.cuda.synchronize()
+    for i in range(16):
+        env.step_device(None, obs_out=ring[i % T], reward_out=rew[i % T], done_out=done[i % T])
     torch.cuda.synchronize()
     x = torch.empty(1 << 28, dtype=torch.float32, device="cuda").uniform_()
     y = torch.empty_like(x)

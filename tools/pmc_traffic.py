@@ -39,13 +39,22 @@ def main():
     copy = [k for k in f if "copyBuffer" in k]
     copy_bytes = float(1 << 30)
     factor = copy_bytes / statistics.median(f[copy[0]]) if copy else 2.0
-    fetch_raw = statistics.median(f[step][3:])  # skip warm-up launches
-    write = statistics.median(w[step][3:])
+    # the last 16 launches are the timed-step workload (earlier ones: the stagger setup)
+    fetch_raw = statistics.median(f[step][-13:])
+    write = statistics.median(w[step][-13:])
+    rs = [k for k in f if "k_reset_listed" in k]
+    reset = None
+    if rs:
+        rf, rw = statistics.median(f[rs[0]][-13:]) * factor, statistics.median(w[rs[0]][-13:])
+        reset = dict(kernel=rs[0], read_bytes=rf, write_bytes=rw, hbm_bytes_per_launch=rf + rw)
     res = dict(config=args.config, envs=args.envs, kernel=step,
                fetch_size_raw_bytes=fetch_raw, fetch_correction=factor,
                read_bytes=fetch_raw * factor, write_bytes=write,
                hbm_bytes_per_launch=fetch_raw * factor + write,
                hbm_bytes_per_env_step=(fetch_raw * factor + write) / args.envs,
+               reset_kernel=reset,
+               step_plus_reset_bytes_per_env_step=(fetch_raw * factor + write
+                                                   + (reset["hbm_bytes_per_launch"] if reset else 0.0)) / args.envs,
                calibration="1 GiB device copy: write = %.3f GiB, raw fetch = %.3f GiB" % (
                    statistics.median(w[copy[0]]) / copy_bytes if copy else float("nan"),
                    statistics.median(f[copy[0]]) / copy_bytes if copy else float("nan")))
