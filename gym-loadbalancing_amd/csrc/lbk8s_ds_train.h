@@ -29,6 +29,8 @@
 // 16(k >> 2) + 4(l >> 4) + (k & 3).
 #pragma once
 
+#include <type_traits>
+
 #include "lbk8s_deepsets.h"
 
 namespace lbk {
@@ -55,12 +57,11 @@ enum : int {
     DSV_FLOATS = 648,
 };
 
-constexpr int DSB_BLOCK = 512;                       // 8 waves: 2 per SIMD, one block per CU
+constexpr int DSB_BLOCK = 256;                       // 4 waves: 1 per SIMD, one block per CU
 constexpr int DSW_FLOATS = 4608;                     // per head: dLambda2 [64][64], dLambda1 [64][8]
 constexpr int DSW_GRID = 256;                        // fixed grid (any B): one block per CU
 constexpr int DSW_SLOTS = DSW_GRID;                  // one partial-sum slot per block
 constexpr int DST_STRIDE = 80;                       // LDS transpose row stride (floats)
-constexpr int DSB_LDS_W = 16384;                     // head weights in LDS (the critic's four 64x64)
 
 struct DSBwdParams {
     const float* obs;          // [B][R][8]
@@ -100,21 +101,6 @@ __device__ __forceinline__ TBOff tb_offsets(int col, int grp) {
     return o;
 }
 
-// one 16-row tile of a [B][R][64] plane in fragment layout (lane: row 16t + col, features
-// 16nt + 4grp + i); rows past R read row R - 1 (in bounds, no branch) and are zeroed
-__device__ __forceinline__ void load_tile(const float* plane, float (&h)[16], int64_t env, int R, int row, int grp) {
-    const bool ok = row < R;
-    const float* q = plane + (env * (int64_t)R + (ok ? row : R - 1)) * 64 + 4 * grp;
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-        const float4 v = *reinterpret_cast<const float4*>(q + 16 * nt);
-        h[4 * nt] = ok ? v.x : 0.f;
-        h[4 * nt + 1] = ok ? v.y : 0.f;
-        h[4 * nt + 2] = ok ? v.z : 0.f;
-        h[4 * nt + 3] = ok ? v.w : 0.f;
-    }
-}
-
 // a 16-feature vector in k layout (every lane of a row holds it): column-0 lanes store it
 __device__ __forceinline__ void store_vec(float* dst, const float (&v)[16], int col, int grp) {
     if (col != 0) return;
@@ -130,24 +116,6 @@ __device__ __forceinline__ int id_of(const int (&id)[4], int k) { return (id[k >
 template <int ACT>
 __device__ __forceinline__ float dact(float y) {
     return ACT == 1 ? (y > 0.f ? 1.f : 0.f) : (y > 0.f ? 1.f : y + 1.f);
-}
-
-// per-lane running (max, first row) of a pass-1 sweep -> the set's max and FIRST argmax row
-// (torch.max's index) per feature: the max over the 16 lanes of the row group, then the
-// smallest row among the lanes that hold it
-__device__ __forceinline__ void finish_argmax(float (&m)[16], const float (&r)[16], int (&id)[4]) {
-    float M[16], c[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) M[k] = m[k];
-    row_reduce<true>(M);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) c[k] = m[k] == M[k] ? -r[k] : -1e9f;
-    row_reduce<true>(c);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) m[k] = M[k];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        id[q] = (int)(-c[4 * q]) | ((int)(-c[4 * q + 1]) << 8) | ((int)(-c[4 * q + 2]) << 16) | ((int)(-c[4 * q + 3]) << 24);
 }
 
 // stage one 16-row tile (this lane: row col, features 16nt + 4grp + i) in LDS
@@ -179,41 +147,195 @@ __device__ __forceinline__ void wgrad64(const float* la, const float* lb, dsf4 (
 
 // acc[mt] += dz^T obs over one staged tile (dz1 in la): the tile's observation rows (this
 // lane: features grp and 4 + grp of row col) are staged in lb, B columns 8..15 read as zero
+template <int NC = 4>
 __device__ __forceinline__ void wgrad8(const float* la, float* lb, const float (&x0)[2], dsf4 (&acc)[4], int col,
                                        const TBOff& o) {
     lb[o.w80] = x0[0];
     lb[o.w81] = x0[1];
+    // every operand read before the first MFMA (one LDS wait instead of one per MFMA)
+    float xv[NC], av[NC][4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < NC; ++c) {
         const float x = lb[o.r8 + 320 * c + 16 * (c & 1)];
-        const float xv = col < 8 ? x : 0.f;
+        xv[c] = col < 8 ? x : 0.f;
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) acc[mt] = mfma4(la[o.rd + 320 * c + 16 * (mt ^ (c & 1))], xv, acc[mt]);
+        for (int mt = 0; mt < 4; ++mt) av[c][mt] = la[o.rd + 320 * c + 16 * (mt ^ (c & 1))];
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[mt] = mfma4(av[c][mt], xv[c], acc[mt]);
+}
+
+// ---- the backward kernel
+//
+// One wave per SIMD (4 per CU, 512 registers each).  A wave walks its sets (env0, env0 +
+// nwaves, ...) as one stream of 16-row steps; step t of iteration j runs
+//   pass 1 (VALU) on rows 16t..16t+15 of set j, transposed: lane f owns feature f and
+//     walks the rows in order, so the set-wise max, its FIRST argmax row (torch.max's
+//     index; strict > over ascending rows) and the set sums need no cross-lane reduction;
+//   pass 2 (MFMA) on tile t of set j - 1 (whose set vectors pass 1 finished one iteration
+//     earlier): dz2 from h2; dLambda2 += dz2^T h1 over the tile's rows (a per-wave LDS
+//     transpose); dz1 = (dz2 Lambda2 - [r == argmax] Gamma2^T sum dz2) act'(h1), Lambda2^T
+//     held in registers; dLambda1 += dz1^T obs;
+// in one basic block, so the two passes' independent instruction streams interleave (the
+// vector work issues in the matrix instructions' shadow).  Iteration 0 runs pass 2 on a
+// dummy set with zero set vectors (it adds nothing) and iteration n pass 1 on a dummy whose
+// results are dropped.  Every step loads the next step's rows before it computes (two
+// buffers, used alternately).  Between iterations: pass 2's per-set sums go out (finish2),
+// and pass 1's set vectors (c1, c2, v: below) are built by lane-per-feature matrix-vector
+// products against natural-order weights in LDS (finish1) and re-read in k layout.
+//
+// Per feature o, dz2[r][o] = (c1[o] - [r == argmax] c2[o]) elu'(h2[r][o]) with actor
+// c1 = dl[r] Lambda3[o] (row-dependent through dl), c2 = g3 Gamma3[o], g3 = sum_r dl[r];
+// critic c1 = u[o] = (Lambda3^T dmean)[o] / R, c2 = vv[o] = (Gamma3^T dmean)[o].  Its set
+// sum is closed-form: sum_r dz2[r][o] = c1 S[o] - c2 elu'(max_r h2[r][o]) with
+// S = sum_r w[r] elu'(h2[r][o]) = sum_r w[r] min(h2[r][o], 0) + sum_r w[r] (ELU output y:
+// elu' = y > 0 ? 1 : y + 1), w = dl (actor) / 1 (critic).
+constexpr int DSB_WAVES = DSB_BLOCK / 64;
+constexpr int DSB_NAT = 3 * 4096 + 128;  // natural-order weights (below)
+constexpr int DSB_CV = 384;              // per-wave set vectors (below)
+
+// pass-2 input tile as loaded: rows past R read row R - 1 (finite values, in bounds) and
+// every use masks them, so no instruction touches the registers before the tile is used
+struct Tile2 {
+    float a[16];  // h2 / c2 (lane: row 16t + col, features 16nt + 4grp + i)
+    float h[16];  // h1 / c1
+    float x0[2];  // observation features grp, 4 + grp
+    float d;      // the actor's dlogit
+};
+// pass-1 rows 16t + q (q < 16), lane = feature; rows past R repeat row R - 1 (a repeated
+// row changes no max / first argmax, and gets weight 0 in the sums)
+struct Rows1 {
+    float a[16], h[16];  // h2 / c2, h1 / c1 of feature lane
+    float x[2];          // observation feature lane & 7 of rows 16t + (lane >> 3), + 8
+    float dl;            // the actor's dlogit of row 16t + (lane & 15)
+};
+struct StepIn {
+    Tile2 t2;
+    Rows1 r1;
+};
+
+template <int HEAD>
+__device__ __forceinline__ void load_step(const DSBwdParams& p, const float* in1, const float* in2, int64_t env2,
+                                          int64_t env1, int t, int lane, StepIn& s) {
+    const int R = p.R, col = lane & 15, grp = lane >> 4;
+    {
+        const int64_t er = env2 * (int64_t)R + min(16 * t + col, R - 1);
+        const float* q2 = in2 + er * 64 + 4 * grp;
+        const float* q1 = in1 + er * 64 + 4 * grp;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            const float4 u = *reinterpret_cast<const float4*>(q2 + 16 * nt);
+            const float4 v = *reinterpret_cast<const float4*>(q1 + 16 * nt);
+            s.t2.a[4 * nt] = u.x;
+            s.t2.a[4 * nt + 1] = u.y;
+            s.t2.a[4 * nt + 2] = u.z;
+            s.t2.a[4 * nt + 3] = u.w;
+            s.t2.h[4 * nt] = v.x;
+            s.t2.h[4 * nt + 1] = v.y;
+            s.t2.h[4 * nt + 2] = v.z;
+            s.t2.h[4 * nt + 3] = v.w;
+        }
+        const float* x = p.obs + er * 8;
+        s.t2.x0[0] = x[grp];
+        s.t2.x0[1] = x[4 + grp];
+        s.t2.d = HEAD == 0 ? p.dlogits[er] : 0.f;
+    }
+    {
+        // one wave-uniform base per plane, the rows at immediate offsets
+        const int64_t e0 = env1 * (int64_t)R, rb = e0 + 16 * t;
+        const float* b2 = in2 + rb * 64 + lane;
+        const float* b1 = in1 + rb * 64 + lane;
+        if (16 * t + 16 <= R) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                s.r1.a[q] = b2[q * 64];
+                s.r1.h[q] = b1[q * 64];
+            }
+        } else {
+            const int qmax = R - 1 - 16 * t;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int qq = min(q, qmax);
+                s.r1.a[q] = b2[qq * 64];
+                s.r1.h[q] = b1[qq * 64];
+            }
+        }
+        s.r1.x[0] = p.obs[(e0 + min(16 * t + (lane >> 3), R - 1)) * 8 + (lane & 7)];
+        s.r1.x[1] = p.obs[(e0 + min(16 * t + 8 + (lane >> 3), R - 1)) * 8 + (lane & 7)];
+        s.r1.dl = HEAD == 0 ? p.dlogits[e0 + min(16 * t + col, R - 1)] : 0.f;
     }
 }
 
+// a 16-feature k-layout vector from a 64-float LDS vector (4 broadcast float4 reads)
+__device__ __forceinline__ void read_vec(const float* src, float (&v)[16], int grp) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+        const float4 x = *reinterpret_cast<const float4*>(src + 16 * nt + 4 * grp);
+        v[4 * nt] = x.x;
+        v[4 * nt + 1] = x.y;
+        v[4 * nt + 2] = x.z;
+        v[4 * nt + 3] = x.w;
+    }
+}
+
+// lane-per-feature matrix-vector product out[lane] = sum_i M[i][lane] x[i], M natural
+// order ([i][o], 64 x 64) in LDS, x a 64-float LDS vector (broadcast reads)
+__device__ __forceinline__ float matvec64(const float* M, const float* x, int lane, float xs = 1.f) {
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const float4 v = *reinterpret_cast<const float4*>(x + 4 * j);
+        acc += M[(4 * j) * 64 + lane] * (v.x * xs);
+        acc += M[(4 * j + 1) * 64 + lane] * (v.y * xs);
+        acc += M[(4 * j + 2) * 64 + lane] * (v.z * xs);
+        acc += M[(4 * j + 3) * 64 + lane] * (v.w * xs);
+    }
+    return acc;
+}
+
 // One launch per head (HEAD 0 actor, 1 critic).
-template <int HEAD>
+// NCT: 4-row groups of the last tile that hold set rows (ceil(((R - 1) % 16 + 1) / 4)); the
+// last tile's weight-gradient products skip the groups past R.
+template <int HEAD, int NCT>
 __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
     constexpr int ACT1 = HEAD == 0 ? 1 : 2;  // activation after layer 1: ReLU (actor) / ELU (critic)
-    __shared__ __attribute__((aligned(16))) float W[DSB_LDS_W];
-    __shared__ __attribute__((aligned(16))) float TB[DSB_BLOCK / 64][2][16 * DST_STRIDE];
-    // the head's weights: [0, 8192) Lambda2^T, Gamma2^T (fragment order); the actor's
-    // Lambda3 / Gamma3 rows at 8192 / 8256, the critic's Lambda3^T / Gamma3^T at 8192 / 12288
+    // natural-order weights [i][o] (W[out i][in o]): Gamma2 at 0; the critic's Lambda3,
+    // Gamma3 at 4096, 8192; the actor's Lambda3 / Gamma3 rows at 12288 / 12352
+    __shared__ __attribute__((aligned(16))) float NAT[DSB_NAT];
+    // Lambda2^T in fragment order (the eq-back's A operands)
+    __shared__ __attribute__((aligned(16))) float LT[4096];
+    __shared__ __attribute__((aligned(16))) float TB[DSB_WAVES][2][16 * DST_STRIDE];
+    // per wave: [0,64) broadcast scratch, c1 [64,128), c2 [128,192), v [192,256), argmax
+    // rows as bytes (id2 at byte 1024 + f, id1 at 1088 + f)
+    __shared__ __attribute__((aligned(16))) float CV[DSB_WAVES][DSB_CV];
     {
-        const int n = HEAD == 0 ? 8192 : 16384;
-        const float* src = p.wb + (HEAD == 0 ? DSB_A2LT : DSB_C2LT);
-        for (int i = threadIdx.x * 4; i < n; i += DSB_BLOCK * 4)
-            *reinterpret_cast<float4*>(W + i) = *reinterpret_cast<const float4*>(src + i);
+        // fragment image -> natural order: fragment (nt, k), lane l holds W^T[o][i] with
+        // o = 16nt + (l & 15), i = 16(k >> 2) + 4(l >> 4) + (k & 3)
+        const float* srcs[3] = {p.wb + (HEAD == 0 ? DSB_A2GT : DSB_C2GT), p.wb + DSB_C3LT, p.wb + DSB_C3GT};
+        const int nm = HEAD == 0 ? 1 : 3;
+        for (int idx = threadIdx.x; idx < 4096 * nm; idx += DSB_BLOCK) {
+            const int m = idx >> 12, i = (idx >> 6) & 63, o = idx & 63;
+            const int k = 4 * (i >> 4) + (i & 3), l = (o & 15) + 16 * ((i >> 2) & 3);
+            NAT[idx] = srcs[m][((o >> 4) * 16 + k) * 64 + l];
+        }
         if (HEAD == 0)
-            for (int i = threadIdx.x; i < 128; i += DSB_BLOCK) W[8192 + i] = p.wb[DSB_A3L + i];
+            for (int i = threadIdx.x; i < 128; i += DSB_BLOCK) NAT[12288 + i] = p.wb[DSB_A3L + i];
+        // Lambda2^T fragments regrouped by k quad: LT[((nt * 4 + kq) * 64 + lane) * 4 + kk] is
+        // fragment (nt, 4kq + kk) of lane, one float4 read per (nt, kq)
+        const float* src = p.wb + (HEAD == 0 ? DSB_A2LT : DSB_C2LT);
+        for (int i = threadIdx.x; i < 4096; i += DSB_BLOCK)
+            LT[i] = src[(4 * (i >> 8) + (i & 3)) * 64 + ((i >> 2) & 63)];
     }
     __syncthreads();
-    const float* LT = W;  // (Gamma2^T at W + 4096)
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t nwaves = (int64_t)gridDim.x * (DSB_BLOCK / 64);
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t nwaves = (int64_t)gridDim.x * DSB_WAVES;
     float* la = TB[wv][0];
     float* lb = TB[wv][1];
+    float* cv = CV[wv];
+    uint8_t* cvb = reinterpret_cast<uint8_t*>(cv);
     const int R = p.R, ntl = (R + 15) / 16;
     const int col = lane & 15, grp = lane >> 4;
     const TBOff tbo = tb_offsets(col, grp);
@@ -228,179 +350,224 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
         for (int nt = 0; nt < 4; ++nt) w2[mt][nt] = dsf4{0.f, 0.f, 0.f, 0.f};
         w1[mt] = dsf4{0.f, 0.f, 0.f, 0.f};
     }
-    for (int64_t env = (int64_t)blockIdx.x * (DSB_BLOCK / 64) + wv; env < p.B; env += nwaves) {
-        float* sv = p.setvec + env * DSV_FLOATS;
-        // weights re-read from LDS per set (an opaque offset: no loop-invariant hoisting)
-        uint32_t wso = 0;
-        asm volatile("" : "+s"(wso));
-        const float* Ws = W + wso;
-        // ---- pass 1: set-wise maxima + first argmax rows, set sums
-        float mx2[16], r2[16], mx1[16], r1[16], S[16], G[16], g3 = 0.f;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            mx2[k] = mx1[k] = -INFINITY;
-            r2[k] = r1[k] = 0.f;
-            S[k] = G[k] = 0.f;
-        }
-        for (int t = 0; t < ntl; ++t) {
-            const int row = 16 * t + col;
-            const bool ok = row < R;
-            const float fr = (float)row;
-            float a[16], h[16];
-            load_tile(in2, a, env, R, row, grp);
-            load_tile(in1, h, env, R, row, grp);
-            float w = ok ? 1.f : 0.f;  // actor: dlogit of the row (0 past R); critic: row validity
-            if (HEAD == 0) {
-                const float d = p.dlogits[env * R + (ok ? row : R - 1)];
-                w = ok ? d : 0.f;
-                g3 += w;
-            }
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const bool u2 = ok && a[k] > mx2[k];  // strict: rows ascend, the first maximum stays
-                mx2[k] = u2 ? a[k] : mx2[k];
-                r2[k] = u2 ? fr : r2[k];
-                S[k] += w * dact<2>(a[k]);
-                G[k] += HEAD == 0 ? w * a[k] : a[k];  // actor: sum dl h2 (Lambda3); critic: sum c2
-                const bool u1 = ok && h[k] > mx1[k];
-                mx1[k] = u1 ? h[k] : mx1[k];
-                r1[k] = u1 ? fr : r1[k];
-            }
-        }
-        int id2[4], id1[4];
-        finish_argmax(mx2, r2, id2);
-        finish_argmax(mx1, r1, id1);
-        row_reduce<false>(S);
-        row_reduce<false>(G);
-        store_vec(sv + (HEAD == 0 ? DSV_MAX2A : DSV_MAX2C), mx2, col, grp);
-        store_vec(sv + (HEAD == 0 ? DSV_GA3 : DSV_CS2), G, col, grp);
-        store_vec(sv + (HEAD == 0 ? DSV_MAX1A : DSV_MAX1C), mx1, col, grp);
-        // per feature o, dz2[r][o] = (c1[o] - [r == argmax] c2[o]) elu'(h2[r][o]) with
-        // actor c1 = dl[r] Lambda3[o] (row-dependent through dl), c2 = g3 Gamma3[o];
-        // critic c1 = u[o] = (Lambda3^T dmean)[o] / R, c2 = vv[o] = (Gamma3^T dmean)[o]
-        float c1[16], c2[16];
-        if (HEAD == 0) {
-            float gv[4] = {g3, 0.f, 0.f, 0.f};
-            row_reduce<false>(gv);
-            g3 = gv[0];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const int f = 16 * (k >> 2) + 4 * grp + (k & 3);
-                c1[k] = Ws[8192 + f];
-                c2[k] = g3 * Ws[8256 + f];
-            }
-        } else {
-            float gm[16];
-            const float* q = p.dmean + env * 64 + 4 * grp;
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt) {
-                const float4 v = *reinterpret_cast<const float4*>(q + 16 * nt);
-                gm[4 * nt] = v.x;
-                gm[4 * nt + 1] = v.y;
-                gm[4 * nt + 2] = v.z;
-                gm[4 * nt + 3] = v.w;
-            }
-            const float invR = 1.0f / (float)R;
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt) {
-                dsf4 uu = {0.f, 0.f, 0.f, 0.f}, w = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    uu = mfma4(Ws[8192 + (nt * 16 + k) * 64 + lane], gm[k] * invR, uu);
-                    w = mfma4(Ws[12288 + (nt * 16 + k) * 64 + lane], gm[k], w);
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    c1[4 * nt + i] = uu[i];
-                    c2[4 * nt + i] = w[i];
-                }
-            }
-        }
-        // sum over the set of dz2, in closed form from pass 1's sums (S = sum of dl elu'(h2)
-        // for the actor, of elu'(c2) over the set's rows for the critic)
-        float gs[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) gs[k] = c1[k] * S[k] - c2[k] * dact<2>(mx2[k]);
-        store_vec(sv + (HEAD == 0 ? DSV_GS2A : DSV_GS2C), gs, col, grp);
-        // v = Gamma2^T (sum dz2): the pooled part of the layer-1 data gradient
-        float v[16];
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-            dsf4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int k = 0; k < 16; ++k) acc = mfma4(Ws[4096 + (nt * 16 + k) * 64 + lane], gs[k], acc);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[4 * nt + i] = acc[i];
-        }
-        // ---- pass 2, per tile: dz2, dLambda2 += dz2^T h1, dz1, dLambda1 += dz1^T obs
-        float gs1[16], m0[2] = {-INFINITY, -INFINITY};
+    const int64_t env0 = (int64_t)blockIdx.x * DSB_WAVES + wv;
+    const int64_t n = env0 < p.B ? (p.B - 1 - env0) / nwaves + 1 : 0;  // this wave's sets
+    if (n > 0) {
+        // set vectors of the set pass 2 works on (zero for the dummy, no argmax row)
+        cv[64 + lane] = cv[128 + lane] = cv[192 + lane] = 0.f;
+        cvb[1024 + lane] = cvb[1088 + lane] = 0xff;
+        // pass-1 state (lane = feature) and pass 2's per-set sums
+        float mx2, mx1, S, G, m0, g3, gs1[16];
+        int r2, r1;
+        auto reset1 = [&]() {
+            mx2 = mx1 = m0 = -INFINITY;
+            S = G = g3 = 0.f;
+            r2 = r1 = 0;
+        };
+        reset1();
 #pragma unroll
         for (int k = 0; k < 16; ++k) gs1[k] = 0.f;
-        for (int t = 0; t < ntl; ++t) {
-            // Lambda2^T re-read from LDS per tile: an opaque offset keeps the compiler from
-            // hoisting its 64 loop-invariant fragments into registers (which spilled)
+        auto env_of = [&](int64_t j) { return env0 + j * nwaves; };
+
+        // pass 1 on rows 16t + q0 .. 16t + q0 + 3; wl: the row weights (lane j: row 16t + j),
+        // dl (actor) / 1 (critic), 0 past R
+        auto pass1 = [&](int t, const Rows1& c, float wl, int q0) {
+#pragma clang fp contract(fast)
+#pragma unroll
+            for (int q = q0; q < q0 + 4; ++q) {
+                const int r = 16 * t + q;
+                const float w = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, wl), q));
+                const bool u2 = c.a[q] > mx2;  // strict: rows ascend, the first maximum stays
+                mx2 = u2 ? c.a[q] : mx2;
+                r2 = u2 ? r : r2;
+                S += w * fminf(c.a[q], 0.f);
+                G += w * c.a[q];  // actor: sum dl h2 (Lambda3); critic: sum c2
+                const bool u1 = c.h[q] > mx1;
+                mx1 = u1 ? c.h[q] : mx1;
+                r1 = u1 ? r : r1;
+            }
+        };
+        // one step's work: pass 2 on tile t of the older set, pass 1 on rows 16t.. of the
+        // newer, pass 1's quarters placed between the weight-gradient MFMA groups
+        auto compute = [&](int t, StepIn& s, auto ncc) {
+#pragma clang fp contract(fast)
+            constexpr int NC = decltype(ncc)::value;  // 4-row groups with set rows
+            Tile2& c = s.t2;
+            const float wl = 16 * t + col < R ? (HEAD == 0 ? s.r1.dl : 1.f) : 0.f;
+            if (HEAD == 0) g3 += wl;  // per lane (row 16t + lane & 15); rows summed in finish1
+            // Lambda2^T and the set vectors re-read from LDS per step: an opaque offset keeps
+            // the compiler from hoisting the loop-invariant reads into registers
             uint32_t wo = 0;
             asm volatile("" : "+s"(wo));
             const float* LTt = LT + wo;
-            const int row = 16 * t + col;
-            const bool ok = row < R;
-            float a[16], h[16], x0[2];
-            load_tile(in2, a, env, R, row, grp);
-            load_tile(in1, h, env, R, row, grp);
-            {
-                const float* x = p.obs + (env * (int64_t)R + (ok ? row : R - 1)) * 8;
-                x0[0] = ok ? x[grp] : 0.f;
-                x0[1] = ok ? x[4 + grp] : 0.f;
-            }
-            float d = 0.f;
-            if (HEAD == 0) {
-                const float dv = p.dlogits[env * R + (ok ? row : R - 1)];
-                d = ok ? dv : 0.f;
-            }
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const float x = (HEAD == 0 ? d * c1[k] : c1[k]) - (row == id_of(id2, k) ? c2[k] : 0.f);
-                a[k] = ok ? x * dact<2>(a[k]) : 0.f;
-            }
-            stage_tile(la, a, tbo);
-            stage_tile(lb, h, tbo);
-            wgrad64(la, lb, w2, tbo);
+            const float* cvt = cv + wo;
+            float c1k[16], c2k[16];
+            int id2k[4], id1k[4];
+            read_vec(cvt + 64, c1k, grp);
+            read_vec(cvt + 128, c2k, grp);
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt) {
-                dsf4 acc = {0.f, 0.f, 0.f, 0.f};
+                id2k[nt] = *reinterpret_cast<const int*>(reinterpret_cast<const uint8_t*>(cvt) + 1024 + 16 * nt + 4 * grp);
+                id1k[nt] = *reinterpret_cast<const int*>(reinterpret_cast<const uint8_t*>(cvt) + 1088 + 16 * nt + 4 * grp);
+            }
+            const int row = 16 * t + col;
+            const bool ok = row < R;
+            const float w = ok ? (HEAD == 0 ? c.d : 1.f) : 0.f;
+            // rows past R: w = 0 and their row is never an argmax, so dz2 = dz1 = 0
 #pragma unroll
-                for (int k = 0; k < 16; ++k) acc = mfma4(LTt[(nt * 16 + k) * 64 + lane], a[k], acc);
+            for (int k = 0; k < 16; ++k) {
+                const float x = w * c1k[k] - (row == id_of(id2k, k) ? c2k[k] : 0.f);
+                c.a[k] = x * fminf(c.a[k], 0.f) + x;  // x elu'(h2), elu' = min(y, 0) + 1
+            }
+            stage_tile(la, c.a, tbo);
+            stage_tile(lb, c.h, tbo);
+            // dLambda2 += dz2^T h1 (wgrad64), k-step by k-step, a pass-1 quarter after each
+#pragma unroll
+            for (int cs = 0; cs < 4; ++cs) {
+                float av[4], bv[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const int i = tbo.rd + 320 * cs + 16 * (m ^ (cs & 1));
+                    av[m] = la[i];
+                    bv[m] = lb[i];
+                }
+                if (cs < NC)
+#pragma unroll
+                    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+                        for (int nt = 0; nt < 4; ++nt) w2[mt][nt] = mfma4(av[mt], bv[nt], w2[mt][nt]);
+                pass1(t, s.r1, wl, 4 * cs);
+            }
+            m0 = max2(m0, max2(s.r1.x[0], s.r1.x[1]));
+            float vk[16];
+            read_vec(cvt + 192, vk, grp);
+            // dz1 pre-activation = dz2 Lambda2: the four output tiles' chains interleaved
+            dsf4 eacc[4];
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) eacc[nt] = dsf4{0.f, 0.f, 0.f, 0.f};
+            float4 Lf[4], Ln[4];
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) Ln[nt] = *reinterpret_cast<const float4*>(LTt + (nt * 4 * 64 + lane) * 4);
+#pragma unroll
+            for (int kq = 0; kq < 4; ++kq) {
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt) {
+                    Lf[nt] = Ln[nt];
+                    if (kq < 3) Ln[nt] = *reinterpret_cast<const float4*>(LTt + ((nt * 4 + kq + 1) * 64 + lane) * 4);
+                }
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                    for (int nt = 0; nt < 4; ++nt) {
+                        const float l = kk == 0 ? Lf[nt].x : kk == 1 ? Lf[nt].y : kk == 2 ? Lf[nt].z : Lf[nt].w;
+                        eacc[nt] = mfma4(l, c.a[4 * kq + kk], eacc[nt]);
+                    }
+            }
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                const dsf4 acc = eacc[nt];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int kk = 4 * nt + i;
-                    const float x = acc[i] - (row == id_of(id1, kk) ? v[kk] : 0.f);
-                    h[kk] = ok ? x * dact<ACT1>(h[kk]) : 0.f;
+                    const float x = acc[i] - (row == id_of(id1k, kk) ? vk[kk] : 0.f);
+                    c.h[kk] = ACT1 == 1 ? (c.h[kk] > 0.f ? x : 0.f) : x * fminf(c.h[kk], 0.f) + x;
                 }
             }
 #pragma unroll
-            for (int k = 0; k < 16; ++k) gs1[k] += h[k];
-            if (do_max0 && ok) {
-                m0[0] = max2(m0[0], x0[0]);
-                m0[1] = max2(m0[1], x0[1]);
+            for (int k = 0; k < 16; ++k) gs1[k] += c.h[k];
+            stage_tile(la, c.h, tbo);
+            wgrad8<NC>(la, lb, c.x0, w1, col, tbo);
+        };
+        // pass 2's per-set sums of set j2
+        auto finish2 = [&](int64_t j2) {
+            float* sv = p.setvec + env_of(j2) * DSV_FLOATS;
+            row_reduce<false>(gs1);
+            store_vec(sv + (HEAD == 0 ? DSV_GS1A : DSV_GS1C), gs1, col, grp);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) gs1[k] = 0.f;
+        };
+        // pass 1's outputs of set j1 and the set vectors pass 2 needs for it
+        auto finish1 = [&](int64_t j1) {
+            const int64_t env = env_of(j1);
+            float* sv = p.setvec + env * DSV_FLOATS;
+            sv[(HEAD == 0 ? DSV_MAX2A : DSV_MAX2C) + lane] = mx2;
+            sv[(HEAD == 0 ? DSV_MAX1A : DSV_MAX1C) + lane] = mx1;
+            sv[(HEAD == 0 ? DSV_GA3 : DSV_CS2) + lane] = G;
+            if (do_max0) {
+                // lanes with equal (lane & 7) hold the same observation feature
+                m0 = max2(m0, __shfl_xor(m0, 8));
+                m0 = max2(m0, __shfl_xor(m0, 16));
+                m0 = max2(m0, __shfl_xor(m0, 32));
+                if (lane < 8) sv[DSV_MAX0 + lane] = m0;
             }
-            stage_tile(la, h, tbo);
-            wgrad8(la, lb, x0, w1, col, tbo);
-        }
-        row_reduce<false>(gs1);
-        store_vec(sv + (HEAD == 0 ? DSV_GS1A : DSV_GS1C), gs1, col, grp);
-        if (do_max0) {
-            row_reduce<true>(m0);
-            if (col == 0) {
-                sv[DSV_MAX0 + grp] = m0[0];
-                sv[DSV_MAX0 + 4 + grp] = m0[1];
+            float c1, c2;
+            if (HEAD == 0) {
+                // g3 = sum of the set's dlogits: per lane over its rows, then over 16 lanes
+                float gv[4] = {g3, 0.f, 0.f, 0.f};
+                row_reduce<false>(gv);
+                g3 = gv[0];
+                S += g3;
+                c1 = NAT[12288 + lane];
+                c2 = g3 * NAT[12352 + lane];
+            } else {
+                S += (float)R;
+                cv[lane] = p.dmean[env * 64 + lane];
+                c1 = matvec64(NAT + 4096, cv, lane, 1.0f / (float)R);
+                c2 = matvec64(NAT + 8192, cv, lane);
             }
+            const float gs = c1 * S - c2 * dact<2>(mx2);
+            sv[(HEAD == 0 ? DSV_GS2A : DSV_GS2C) + lane] = gs;
+            cv[64 + lane] = c1;
+            cv[128 + lane] = c2;
+            cvb[1024 + lane] = (uint8_t)r2;
+            cvb[1088 + lane] = (uint8_t)r1;
+            cv[lane] = gs;
+            cv[192 + lane] = matvec64(NAT, cv, lane);  // v = Gamma2^T (sum dz2)
+        };
+
+        // step g = j * ntl + t of the stream, j in [0, n]: pass 1 on set min(j, n - 1),
+        // pass 2 on set max(j - 1, 0)
+        const int64_t steps = (n + 1) * ntl;
+        int64_t j = 0;
+        int t = 0;
+        StepIn A, B;
+        load_step<HEAD>(p, in1, in2, env_of(0), env_of(0), 0, lane, A);
+        auto step = [&](StepIn& cur, StepIn& nxt, bool more) {
+            int tn = t + 1;
+            int64_t jn = j;
+            if (tn == ntl) {
+                tn = 0;
+                ++jn;
+            }
+            if (more)
+                load_step<HEAD>(p, in1, in2, env_of(jn > 0 ? jn - 1 : 0), env_of(jn < n ? jn : n - 1), tn, lane, nxt);
+            if (NCT < 4 && t == ntl - 1)
+                compute(t, cur, std::integral_constant<int, NCT>{});
+            else
+                compute(t, cur, std::integral_constant<int, 4>{});
+            if (tn == 0) {
+                if (j > 0) finish2(j - 1);
+                else {
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) gs1[k] = 0.f;
+                }
+                if (j < n) finish1(j);
+                reset1();
+            }
+            t = tn;
+            j = jn;
+        };
+        for (int64_t g = 0; g + 1 < steps; g += 2) {
+            step(A, B, true);
+            step(B, A, g + 2 < steps);
         }
+        if (steps & 1) step(A, B, false);
     }
-    // the block's 8 waves summed in LDS in a fixed order, one slot per block
+    // the block's waves summed in LDS in a fixed order, one slot per block
     __syncthreads();
     float* red = &TB[0][0][0];
     static_assert(sizeof(TB) / sizeof(float) >= DSW_FLOATS, "reduction buffer");
-    for (int w = 0; w < DSB_BLOCK / 64; ++w) {
+    for (int w = 0; w < DSB_WAVES; ++w) {
         if (wv == w) {
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt)

@@ -125,6 +125,36 @@ __device__ __forceinline__ void slice_write_obs(const Params& p, float* out, int
     }
 }
 
+// get_state() for the 4 envs of a wave (W = 16) as ONE contiguous run: the envs' R x 32-byte
+// blocks are consecutive, so the wave's 4 blocks are 128·R bytes starting at a multiple of
+// 128·R (envs 4w .. 4w + 3): every store instruction covers whole 128-byte lines.  Per-env
+// runs started mid-line (R x 32 B = 2,080 B at E = 64), and the nontemporal stores reached
+// HBM as partial lines.  The rows go through a per-wave LDS image (wave-local: LDS
+// instructions of one wave complete in order).  Only for full waves (env0 + 4 <= B).
+template <int EPL>
+__device__ __forceinline__ void slice_write_obs_wave(const Params& p, float* out, int64_t env0, int wl,
+                                                     const SEnv<EPL>& v, float4* st) {
+    constexpr int W = 16;
+    const int el = wl / W, lane = wl % W, n4 = 2 * p.R;
+    const float rz = (float)v.s.rz, thr = (float)threshold(v.s.thr_idx), dt = (float)v.dt;
+    float4* mine = st + el * n4;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+        const int r = lane + k * W;
+        if (r < p.E) {
+            const int z = em_zone(v.em[k]);
+            mine[2 * r] = make_float4((float)z, (float)zcap_val(v.zcap, z), v.ocpu[k], (float)topo_val(v.topo, z, v.s.rz));
+            mine[2 * r + 1] = make_float4(v.olat[k], rz, thr, dt);
+        }
+    }
+    if (lane == 0 && p.R > p.E) {  // the reject row
+        mine[2 * p.E] = make_float4(-1.f, -1.f, -1.f, -1.f);
+        mine[2 * p.E + 1] = make_float4(-1.f, rz, thr, dt);
+    }
+    float4* base = reinterpret_cast<float4*>(out + env0 * (int64_t)p.R * 8);
+    for (int f = wl; f < 4 * n4; f += 64) st_stream(base + f, st[f]);
+}
+
 template <int W, int EPL>
 __device__ __forceinline__ void slice_load(const Params& p, int64_t env, int lane, SEnv<EPL>& v) {
 #pragma unroll
@@ -438,7 +468,19 @@ __device__ __forceinline__ void slice_step_body(const Params& p, int64_t env, in
             if (e == ai || e == oA) p.edyn[eidx(p, env, e)] = v.ed[k];
         }
     }
-    if (obs_out) slice_write_obs<W, EPL>(p, obs_out, env, lane, v);
+    if (obs_out) {
+        if constexpr (W == 16) {
+            // whole-line stores of the wave's 4 envs when all 4 are live
+            __shared__ float4 obs_stage[BLOCK / 64][8 * (16 * EPL + 1)];
+            const int wl = threadIdx.x & 63;
+            const int64_t env0 = env - wl / W;
+            if (env0 + 4 <= p.B) {
+                slice_write_obs_wave<EPL>(p, obs_out, env0, wl, v, obs_stage[threadIdx.x >> 6]);
+                return;
+            }
+        }
+        slice_write_obs<W, EPL>(p, obs_out, env, lane, v);
+    }
 }
 
 // step() (:403-513) fused with next_request(), get_state(), reward, done and auto-reset.

@@ -36,7 +36,11 @@ def main():
     ap.add_argument("--config2", action="store_true")
     ap.add_argument("--config1", action="store_true")
     ap.add_argument("--rollout", action="store_true")
+    ap.add_argument("--lib", default=None, help="another build of liblbk8s.so (A/B)")
     args = ap.parse_args()
+    if args.lib:
+        from lbk8s import _native
+        _native.LIB_PATH = os.path.abspath(args.lib)
     import torch
 
     from lbk8s import LBVecEnv

@@ -17,6 +17,9 @@ from lbk8s import LBVecEnv  # noqa: E402
 
 def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "default"
+    if os.environ.get("PMC_LIB"):  # A/B: another build of liblbk8s.so
+        from lbk8s import _native
+        _native.LIB_PATH = os.path.abspath(os.environ["PMC_LIB"])
     from bench import CONFIGS
     B = int(os.environ.get("PMC_ENVS", 1 << 20))
     env = LBVecEnv(B, seed=0, as_tensors=True, **CONFIGS[cfg])
