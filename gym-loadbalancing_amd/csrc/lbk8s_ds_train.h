@@ -8,25 +8,23 @@
 //   * k_deepsets_fwd<TS, P, true> (lbk8s_deepsets.h) writes the logits, the critic's psi
 //     mean and the hidden activations h1, h2 (actor) / c1, c2 (critic) row-major.
 //   * torch evaluates rho, the PPO loss and its gradient w.r.t. logits and psi mean.
-//   * k_ds_train_bwd (here), one wave per set, 8 waves per CU (2 per SIMD, so one wave's
-//     vector work runs beside the other's matrix work), the set streamed 16 rows at a time
-//     in two passes:
-//       pass 1 (h2, h1): every set-wise max and its FIRST argmax row (torch.max's index)
-//         in one sweep, the set sums the Gamma / Lambda3 gradients need, and the set sum
-//         of dz2 in closed form: sum_r dz2[r][o] = Lambda3[o] sum_r dl[r] elu'(h2[r][o])
-//         - g3 Gamma3[o] elu'(max_r h2[r][o]) (the critic: u, vv for Lambda3, Gamma3);
-//       pass 2, per 16-row tile: dz2 from h2; dLambda2 += dz2^T h1 (MFMA over rows: the
-//         tiles go through a per-wave LDS transpose); the data gradient dz1 = (dz2
-//         Lambda2 - [r == argmax] Gamma2^T sum dz2) act'(h1) (f32 MFMA); dLambda1 += dz1^T obs.
+//   * k_ds_train_bwd (here), one launch per head: each wave (one per SIMD) walks its
+//     sets in 16-row steps, pass 1 of one set beside pass 2 of the previous (below):
+//       pass 1 (h2, h1; VALU, lane = feature): every set-wise max and its FIRST argmax row
+//         (torch.max's index), the set sums the Gamma / Lambda3 gradients need, and the
+//         set sum of dz2 in closed form: sum_r dz2[r][o] = Lambda3[o] sum_r dl[r]
+//         elu'(h2[r][o]) - g3 Gamma3[o] elu'(max_r h2[r][o]) (the critic: u, vv);
+//       pass 2 (MFMA), per 16-row tile: dz2 from h2; dLambda2 += dz2^T h1 over the rows;
+//         the data gradient dz1 = (dz2 Lambda2 - [r == argmax] Gamma2^T sum dz2) act'(h1);
+//         dLambda1 += dz1^T obs.
 //     The weight-gradient accumulators stay in registers across all the sets a wave
-//     visits; at the end the block sums its 8 waves in LDS in a fixed order and writes one
+//     visits; at the end the block sums its waves in LDS in a fixed order and writes one
 //     slot, and k_ds_wgrad_reduce sums the slots in a fixed order: no per-row gradient
 //     reaches HBM, and the result does not depend on timing.  Per-set vectors (set-wise
 //     max, gradient sums over the set, the last-layer products) give every Gamma gradient
 //     and the rank-1 last-layer gradients as small GEMMs over the sets.
-// Layout conventions (fragment order, accumulator layout) are those of lbk8s_deepsets.h:
-// lane l holds set element (l & 15) of each 16-row tile, and at k-step k the features
-// 16(k >> 2) + 4(l >> 4) + (k & 3).
+// Fragment order of the weight image is that of lbk8s_deepsets.h (at k-step k, lane l
+// holds features 16(k >> 2) + 4(l >> 4) + (k & 3)).
 #pragma once
 
 #include <type_traits>
@@ -61,7 +59,7 @@ constexpr int DSB_BLOCK = 256;                       // 4 waves: 1 per SIMD, one
 constexpr int DSW_FLOATS = 4608;                     // per head: dLambda2 [64][64], dLambda1 [64][8]
 constexpr int DSW_GRID = 256;                        // fixed grid (any B): one block per CU
 constexpr int DSW_SLOTS = DSW_GRID;                  // one partial-sum slot per block
-constexpr int DST_STRIDE = 80;                       // LDS transpose row stride (floats)
+constexpr int DST_FLOATS = 1280;                     // per-wave LDS tile buffer (floats)
 
 struct DSBwdParams {
     const float* obs;          // [B][R][8]
@@ -77,94 +75,10 @@ struct DSBwdParams {
     int actor, critic;
 };
 
-// element (row, feature f) of a staged 16-row tile: rows 80 floats apart, the feature index
-// XOR-swizzled by 4 (row & 7) (groups of 4 features stay contiguous), so the row-major
-// float4 stores of 8 consecutive rows and the transposed reads (4 rows x 16 features per
-// 32 lanes) are bank-conflict free.  TBOff holds that index for each access pattern in
-// closed form: a few lane offsets, the rest compile-time constants.
-struct TBOff {
-    int rd;        // transposed reads, row 4c + grp, feature col + 16m:  rd + 320c + 16 (m ^ (c & 1))
-    int we, wo;    // row-major float4 stores, row col, features 16nt + 4grp:  (nt even ? we : wo) + 16nt
-    int w80, w81;  // observation stores, row col, feature 4kk + grp (kk = 0, 1)
-    int r8;        // observation reads, row 4c + grp, feature col & 7:  r8 + 320c + 16 (c & 1)
-};
-__device__ __forceinline__ TBOff tb_offsets(int col, int grp) {
-    static_assert(DST_STRIDE == 80, "closed forms assume 80-float rows");
-    TBOff o;
-    const int b = (col >> 2) & 1, base0 = col * DST_STRIDE + 4 * (grp ^ (col & 3));
-    o.rd = grp * DST_STRIDE + (col ^ (4 * grp));
-    o.we = base0 + 16 * b;
-    o.wo = base0 - 16 * b;
-    o.w80 = col * DST_STRIDE + grp + 4 * (col & 7);
-    o.w81 = col * DST_STRIDE + grp + 4 * (1 ^ (col & 7));
-    o.r8 = grp * DST_STRIDE + ((col & 7) ^ (4 * grp));
-    return o;
-}
-
-// a 16-feature vector in k layout (every lane of a row holds it): column-0 lanes store it
-__device__ __forceinline__ void store_vec(float* dst, const float (&v)[16], int col, int grp) {
-    if (col != 0) return;
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-        *reinterpret_cast<float4*>(dst + 16 * nt + 4 * grp) = make_float4(v[4 * nt], v[4 * nt + 1], v[4 * nt + 2], v[4 * nt + 3]);
-}
-
-// argmax rows (< 80) of 16 features, one byte each: id[k >> 2] byte (k & 3)
-__device__ __forceinline__ int id_of(const int (&id)[4], int k) { return (id[k >> 2] >> (8 * (k & 3))) & 0xff; }
-
 // d act / d z from the activation's output: ReLU (ACT 1) y > 0; ELU (ACT 2) y > 0 ? 1 : y + 1
 template <int ACT>
 __device__ __forceinline__ float dact(float y) {
     return ACT == 1 ? (y > 0.f ? 1.f : 0.f) : (y > 0.f ? 1.f : y + 1.f);
-}
-
-// stage one 16-row tile (this lane: row col, features 16nt + 4grp + i) in LDS
-__device__ __forceinline__ void stage_tile(float* buf, const float (&v)[16], const TBOff& o) {
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-        *reinterpret_cast<float4*>(buf + (nt % 2 == 0 ? o.we : o.wo) + 16 * nt) =
-            make_float4(v[4 * nt], v[4 * nt + 1], v[4 * nt + 2], v[4 * nt + 3]);
-}
-
-// acc[mt][nt] += dz^T h over one staged 16-row tile: MFMA k-step c contracts rows
-// 4c..4c+3; A[m][kk] = dz[4c + kk][16mt + m], B[kk][n] = h[4c + kk][16nt + n]
-__device__ __forceinline__ void wgrad64(const float* la, const float* lb, dsf4 (&acc)[4][4], const TBOff& o) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        float av[4], bv[4];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const int i = o.rd + 320 * c + 16 * (m ^ (c & 1));
-            av[m] = la[i];
-            bv[m] = lb[i];
-        }
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma4(av[mt], bv[nt], acc[mt][nt]);
-    }
-}
-
-// acc[mt] += dz^T obs over one staged tile (dz1 in la): the tile's observation rows (this
-// lane: features grp and 4 + grp of row col) are staged in lb, B columns 8..15 read as zero
-template <int NC = 4>
-__device__ __forceinline__ void wgrad8(const float* la, float* lb, const float (&x0)[2], dsf4 (&acc)[4], int col,
-                                       const TBOff& o) {
-    lb[o.w80] = x0[0];
-    lb[o.w81] = x0[1];
-    // every operand read before the first MFMA (one LDS wait instead of one per MFMA)
-    float xv[NC], av[NC][4];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-        const float x = lb[o.r8 + 320 * c + 16 * (c & 1)];
-        xv[c] = col < 8 ? x : 0.f;
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) av[c][mt] = la[o.rd + 320 * c + 16 * (mt ^ (c & 1))];
-    }
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) acc[mt] = mfma4(av[c][mt], xv[c], acc[mt]);
 }
 
 // ---- the backward kernel
@@ -172,37 +86,41 @@ __device__ __forceinline__ void wgrad8(const float* la, float* lb, const float (
 // One wave per SIMD (4 per CU, 512 registers each).  A wave walks its sets (env0, env0 +
 // nwaves, ...) as one stream of 16-row steps; step t of iteration j runs
 //   pass 1 (VALU) on rows 16t..16t+15 of set j, transposed: lane f owns feature f and
-//     walks the rows in order, so the set-wise max, its FIRST argmax row (torch.max's
-//     index; strict > over ascending rows) and the set sums need no cross-lane reduction;
+//     walks the rows in order, so the set-wise max, its FIRST argmax row (strict > over
+//     ascending rows) and the set sums need no cross-lane reduction;
 //   pass 2 (MFMA) on tile t of set j - 1 (whose set vectors pass 1 finished one iteration
-//     earlier): dz2 from h2; dLambda2 += dz2^T h1 over the tile's rows (a per-wave LDS
-//     transpose); dz1 = (dz2 Lambda2 - [r == argmax] Gamma2^T sum dz2) act'(h1), Lambda2^T
-//     held in registers; dLambda1 += dz1^T obs;
-// in one basic block, so the two passes' independent instruction streams interleave (the
-// vector work issues in the matrix instructions' shadow).  Iteration 0 runs pass 2 on a
-// dummy set with zero set vectors (it adds nothing) and iteration n pass 1 on a dummy whose
-// results are dropped.  Every step loads the next step's rows before it computes (two
-// buffers, used alternately).  Between iterations: pass 2's per-set sums go out (finish2),
-// and pass 1's set vectors (c1, c2, v: below) are built by lane-per-feature matrix-vector
-// products against natural-order weights in LDS (finish1) and re-read in k layout.
+//     earlier), in the W layout: lane (col, grp) holds rows 4c + grp (c < 4) and features
+//     4col .. 4col + 3, which is the operand layout of dLambda2 += dz2^T h1 and dLambda1 +=
+//     dz1^T obs (contraction over rows), so those MFMAs read registers.  The data gradient
+//     (contraction over features, dz1 = dz2 Lambda2, Lambda2^T from LDS) needs rows in the
+//     other index: dz2 goes through a per-wave LDS transpose into it and dz1 back;
+// in one basic block, with pass 1's quarters between the dLambda2 k-steps, so the vector
+// work issues in the matrix instructions' shadow.  Iteration 0 runs pass 2 on a dummy set
+// with zero set vectors (it adds nothing) and iteration n pass 1 on a dummy whose results
+// are dropped.  Every step loads the next step's rows before it computes (two buffers,
+// used alternately).  Between iterations: pass 2's per-set sums go out (finish2), and
+// pass 1's set vectors (c1, c2, v: below) are built by lane-per-feature matrix-vector
+// products against natural-order weights in LDS (finish1).
 //
 // Per feature o, dz2[r][o] = (c1[o] - [r == argmax] c2[o]) elu'(h2[r][o]) with actor
 // c1 = dl[r] Lambda3[o] (row-dependent through dl), c2 = g3 Gamma3[o], g3 = sum_r dl[r];
 // critic c1 = u[o] = (Lambda3^T dmean)[o] / R, c2 = vv[o] = (Gamma3^T dmean)[o].  Its set
 // sum is closed-form: sum_r dz2[r][o] = c1 S[o] - c2 elu'(max_r h2[r][o]) with
 // S = sum_r w[r] elu'(h2[r][o]) = sum_r w[r] min(h2[r][o], 0) + sum_r w[r] (ELU output y:
-// elu' = y > 0 ? 1 : y + 1), w = dl (actor) / 1 (critic).
+// elu' = y > 0 ? 1 : y + 1 = min(y, 0) + 1), w = dl (actor) / 1 (critic).
 constexpr int DSB_WAVES = DSB_BLOCK / 64;
 constexpr int DSB_NAT = 3 * 4096 + 128;  // natural-order weights (below)
 constexpr int DSB_CV = 384;              // per-wave set vectors (below)
 
 // pass-2 input tile as loaded: rows past R read row R - 1 (finite values, in bounds) and
 // every use masks them, so no instruction touches the registers before the tile is used
+// W layout (the weight-gradient MFMAs' operand layout): lane (col, grp) holds, for each
+// 4-row group c, row 16t + 4c + grp and features 4col .. 4col + 3 (one float4)
 struct Tile2 {
-    float a[16];  // h2 / c2 (lane: row 16t + col, features 16nt + 4grp + i)
-    float h[16];  // h1 / c1
-    float x0[2];  // observation features grp, 4 + grp
-    float d;      // the actor's dlogit
+    float4 a[4];  // h2 / c2
+    float4 h[4];  // h1 / c1
+    float x[4];   // observation feature col & 7 of row 16t + 4c + grp
+    float d[4];   // the actor's dlogit of row 16t + 4c + grp
 };
 // pass-1 rows 16t + q (q < 16), lane = feature; rows past R repeat row R - 1 (a repeated
 // row changes no max / first argmax, and gets weight 0 in the sums)
@@ -220,27 +138,13 @@ template <int HEAD>
 __device__ __forceinline__ void load_step(const DSBwdParams& p, const float* in1, const float* in2, int64_t env2,
                                           int64_t env1, int t, int lane, StepIn& s) {
     const int R = p.R, col = lane & 15, grp = lane >> 4;
-    {
-        const int64_t er = env2 * (int64_t)R + min(16 * t + col, R - 1);
-        const float* q2 = in2 + er * 64 + 4 * grp;
-        const float* q1 = in1 + er * 64 + 4 * grp;
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-            const float4 u = *reinterpret_cast<const float4*>(q2 + 16 * nt);
-            const float4 v = *reinterpret_cast<const float4*>(q1 + 16 * nt);
-            s.t2.a[4 * nt] = u.x;
-            s.t2.a[4 * nt + 1] = u.y;
-            s.t2.a[4 * nt + 2] = u.z;
-            s.t2.a[4 * nt + 3] = u.w;
-            s.t2.h[4 * nt] = v.x;
-            s.t2.h[4 * nt + 1] = v.y;
-            s.t2.h[4 * nt + 2] = v.z;
-            s.t2.h[4 * nt + 3] = v.w;
-        }
-        const float* x = p.obs + er * 8;
-        s.t2.x0[0] = x[grp];
-        s.t2.x0[1] = x[4 + grp];
-        s.t2.d = HEAD == 0 ? p.dlogits[er] : 0.f;
+    for (int c = 0; c < 4; ++c) {
+        const int64_t er = env2 * (int64_t)R + min(16 * t + 4 * c + grp, R - 1);
+        s.t2.a[c] = *reinterpret_cast<const float4*>(in2 + er * 64 + 4 * col);
+        s.t2.h[c] = *reinterpret_cast<const float4*>(in1 + er * 64 + 4 * col);
+        s.t2.x[c] = p.obs[er * 8 + (col & 7)];
+        s.t2.d[c] = HEAD == 0 ? p.dlogits[er] : 0.f;
     }
     {
         // one wave-uniform base per plane, the rows at immediate offsets
@@ -265,18 +169,6 @@ __device__ __forceinline__ void load_step(const DSBwdParams& p, const float* in1
         s.r1.x[0] = p.obs[(e0 + min(16 * t + (lane >> 3), R - 1)) * 8 + (lane & 7)];
         s.r1.x[1] = p.obs[(e0 + min(16 * t + 8 + (lane >> 3), R - 1)) * 8 + (lane & 7)];
         s.r1.dl = HEAD == 0 ? p.dlogits[e0 + min(16 * t + col, R - 1)] : 0.f;
-    }
-}
-
-// a 16-feature k-layout vector from a 64-float LDS vector (4 broadcast float4 reads)
-__device__ __forceinline__ void read_vec(const float* src, float (&v)[16], int grp) {
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-        const float4 x = *reinterpret_cast<const float4*>(src + 16 * nt + 4 * grp);
-        v[4 * nt] = x.x;
-        v[4 * nt + 1] = x.y;
-        v[4 * nt + 2] = x.z;
-        v[4 * nt + 3] = x.w;
     }
 }
 
@@ -306,7 +198,8 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
     __shared__ __attribute__((aligned(16))) float NAT[DSB_NAT];
     // Lambda2^T in fragment order (the eq-back's A operands)
     __shared__ __attribute__((aligned(16))) float LT[4096];
-    __shared__ __attribute__((aligned(16))) float TB[DSB_WAVES][2][16 * DST_STRIDE];
+    // per wave: the 16-row tile transposes (16 x 16 float4), and the block's reduction
+    __shared__ __attribute__((aligned(16))) float TB[DSB_WAVES][DST_FLOATS];
     // per wave: [0,64) broadcast scratch, c1 [64,128), c2 [128,192), v [192,256), argmax
     // rows as bytes (id2 at byte 1024 + f, id1 at 1088 + f)
     __shared__ __attribute__((aligned(16))) float CV[DSB_WAVES][DSB_CV];
@@ -332,13 +225,11 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t nwaves = (int64_t)gridDim.x * DSB_WAVES;
-    float* la = TB[wv][0];
-    float* lb = TB[wv][1];
+    float* la = TB[wv];
     float* cv = CV[wv];
     uint8_t* cvb = reinterpret_cast<uint8_t*>(cv);
     const int R = p.R, ntl = (R + 15) / 16;
     const int col = lane & 15, grp = lane >> 4;
-    const TBOff tbo = tb_offsets(col, grp);
     const int64_t plane = p.B * (int64_t)R * 64;
     const float* in1 = HEAD == 0 ? p.save_actor : p.save_critic;  // h1 / c1
     const float* in2 = in1 + plane;                                 // h2 / c2
@@ -357,7 +248,7 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
         cv[64 + lane] = cv[128 + lane] = cv[192 + lane] = 0.f;
         cvb[1024 + lane] = cvb[1088 + lane] = 0xff;
         // pass-1 state (lane = feature) and pass 2's per-set sums
-        float mx2, mx1, S, G, m0, g3, gs1[16];
+        float mx2, mx1, S, G, m0, g3, gs1[4];
         int r2, r1;
         auto reset1 = [&]() {
             mx2 = mx1 = m0 = -INFINITY;
@@ -366,7 +257,7 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
         };
         reset1();
 #pragma unroll
-        for (int k = 0; k < 16; ++k) gs1[k] = 0.f;
+        for (int m = 0; m < 4; ++m) gs1[m] = 0.f;
         auto env_of = [&](int64_t j) { return env0 + j * nwaves; };
 
         // pass 1 on rows 16t + q0 .. 16t + q0 + 3; wl: the row weights (lane j: row 16t + j),
@@ -401,36 +292,40 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
             asm volatile("" : "+s"(wo));
             const float* LTt = LT + wo;
             const float* cvt = cv + wo;
-            float c1k[16], c2k[16];
-            int id2k[4], id1k[4];
-            read_vec(cvt + 64, c1k, grp);
-            read_vec(cvt + 128, c2k, grp);
+            // set vectors of features 4col .. 4col + 3 (W layout)
+            const float4 c1v = *reinterpret_cast<const float4*>(cvt + 64 + 4 * col);
+            const float4 c2v = *reinterpret_cast<const float4*>(cvt + 128 + 4 * col);
+            const int id2w = *reinterpret_cast<const int*>(reinterpret_cast<const uint8_t*>(cvt) + 1024 + 4 * col);
+            // dz2 = (w c1 - [r == argmax] c2) elu'(h2), elu' = min(y, 0) + 1; rows past R have
+            // w = 0 and are never an argmax, so their dz2 (and dz1) is 0
+            float4 dz[4];
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt) {
-                id2k[nt] = *reinterpret_cast<const int*>(reinterpret_cast<const uint8_t*>(cvt) + 1024 + 16 * nt + 4 * grp);
-                id1k[nt] = *reinterpret_cast<const int*>(reinterpret_cast<const uint8_t*>(cvt) + 1088 + 16 * nt + 4 * grp);
-            }
-            const int row = 16 * t + col;
-            const bool ok = row < R;
-            const float w = ok ? (HEAD == 0 ? c.d : 1.f) : 0.f;
-            // rows past R: w = 0 and their row is never an argmax, so dz2 = dz1 = 0
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const float x = w * c1k[k] - (row == id_of(id2k, k) ? c2k[k] : 0.f);
-                c.a[k] = x * fminf(c.a[k], 0.f) + x;  // x elu'(h2), elu' = min(y, 0) + 1
-            }
-            stage_tile(la, c.a, tbo);
-            stage_tile(lb, c.h, tbo);
-            // dLambda2 += dz2^T h1 (wgrad64), k-step by k-step, a pass-1 quarter after each
-#pragma unroll
-            for (int cs = 0; cs < 4; ++cs) {
-                float av[4], bv[4];
+            for (int cc = 0; cc < 4; ++cc) {
+                const int row = 16 * t + 4 * cc + grp;
+                const float w = row < R ? (HEAD == 0 ? c.d[cc] : 1.f) : 0.f;
+                float x[4], y[4] = {c.a[cc].x, c.a[cc].y, c.a[cc].z, c.a[cc].w};
+                const float c1a[4] = {c1v.x, c1v.y, c1v.z, c1v.w}, c2a[4] = {c2v.x, c2v.y, c2v.z, c2v.w};
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
-                    const int i = tbo.rd + 320 * cs + 16 * (m ^ (cs & 1));
-                    av[m] = la[i];
-                    bv[m] = lb[i];
+                    const float u = w * c1a[m] - (row == ((id2w >> (8 * m)) & 0xff) ? c2a[m] : 0.f);
+                    x[m] = u * fminf(y[m], 0.f) + u;
                 }
+                dz[cc] = make_float4(x[0], x[1], x[2], x[3]);
+            }
+            // the tile through LDS into the eq-back's k layout (row = col): float4 q of row rho
+            // at rho * 16 + (q ^ rho), conflict-free both ways
+            float4* T4 = reinterpret_cast<float4*>(la);
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) {
+                const int rho = 4 * cc + grp;
+                T4[rho * 16 + (col ^ rho)] = dz[cc];
+            }
+            // dLambda2 += dz2^T h1 straight from registers (W layout = the MFMA operands),
+            // k-step by k-step, a pass-1 quarter after each
+#pragma unroll
+            for (int cs = 0; cs < 4; ++cs) {
+                const float av[4] = {dz[cs].x, dz[cs].y, dz[cs].z, dz[cs].w};
+                const float bv[4] = {c.h[cs].x, c.h[cs].y, c.h[cs].z, c.h[cs].w};
                 if (cs < NC)
 #pragma unroll
                     for (int mt = 0; mt < 4; ++mt)
@@ -439,8 +334,16 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
                 pass1(t, s.r1, wl, 4 * cs);
             }
             m0 = max2(m0, max2(s.r1.x[0], s.r1.x[1]));
-            float vk[16];
-            read_vec(cvt + 192, vk, grp);
+            // dz2 in k layout (lane: row col, features 16q + 4grp .. + 3 at k = 4q ..)
+            float dk[16];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 v = T4[col * 16 + ((4 * q + grp) ^ col)];
+                dk[4 * q] = v.x;
+                dk[4 * q + 1] = v.y;
+                dk[4 * q + 2] = v.z;
+                dk[4 * q + 3] = v.w;
+            }
             // dz1 pre-activation = dz2 Lambda2: the four output tiles' chains interleaved
             dsf4 eacc[4];
 #pragma unroll
@@ -460,31 +363,53 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
 #pragma unroll
                     for (int nt = 0; nt < 4; ++nt) {
                         const float l = kk == 0 ? Lf[nt].x : kk == 1 ? Lf[nt].y : kk == 2 ? Lf[nt].z : Lf[nt].w;
-                        eacc[nt] = mfma4(l, c.a[4 * kq + kk], eacc[nt]);
+                        eacc[nt] = mfma4(l, dk[4 * kq + kk], eacc[nt]);
                     }
             }
+            // back to the W layout: output tile nt, lane (row col, grp) holds features
+            // 16nt + 4grp .. + 3 = float4 q = 4nt + grp of row col
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt) {
-                const dsf4 acc = eacc[nt];
+            for (int nt = 0; nt < 4; ++nt)
+                T4[col * 16 + ((4 * nt + grp) ^ col)] = make_float4(eacc[nt][0], eacc[nt][1], eacc[nt][2], eacc[nt][3]);
+            const float4 vv = *reinterpret_cast<const float4*>(cvt + 192 + 4 * col);
+            const int id1w = *reinterpret_cast<const int*>(reinterpret_cast<const uint8_t*>(cvt) + 1088 + 4 * col);
+            const float va[4] = {vv.x, vv.y, vv.z, vv.w};
+            // dz1 = (pre - [r == argmax] Gamma2^T sum dz2) act'(h1), W layout; its set sum;
+            // dLambda1 += dz1^T obs (B columns 8..15 zero)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int kk = 4 * nt + i;
-                    const float x = acc[i] - (row == id_of(id1k, kk) ? vk[kk] : 0.f);
-                    c.h[kk] = ACT1 == 1 ? (c.h[kk] > 0.f ? x : 0.f) : x * fminf(c.h[kk], 0.f) + x;
+            for (int cc = 0; cc < 4; ++cc) {
+                const int rho = 4 * cc + grp, row = 16 * t + rho;
+                const float4 pre = T4[rho * 16 + (col ^ rho)];
+                const float pa[4] = {pre.x, pre.y, pre.z, pre.w};
+                const float ha[4] = {c.h[cc].x, c.h[cc].y, c.h[cc].z, c.h[cc].w};
+                float d1[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const float u = pa[m] - (row == ((id1w >> (8 * m)) & 0xff) ? va[m] : 0.f);
+                    d1[m] = ACT1 == 1 ? (ha[m] > 0.f ? u : 0.f) : u * fminf(ha[m], 0.f) + u;
+                    gs1[m] += d1[m];
+                }
+                if (cc < NC) {
+                    const float xv = col < 8 ? c.x[cc] : 0.f;
+#pragma unroll
+                    for (int mt = 0; mt < 4; ++mt) w1[mt] = mfma4(d1[mt], xv, w1[mt]);
                 }
             }
-#pragma unroll
-            for (int k = 0; k < 16; ++k) gs1[k] += c.h[k];
-            stage_tile(la, c.h, tbo);
-            wgrad8<NC>(la, lb, c.x0, w1, col, tbo);
         };
         // pass 2's per-set sums of set j2
         auto finish2 = [&](int64_t j2) {
             float* sv = p.setvec + env_of(j2) * DSV_FLOATS;
-            row_reduce<false>(gs1);
-            store_vec(sv + (HEAD == 0 ? DSV_GS1A : DSV_GS1C), gs1, col, grp);
+            // the four row groups (lanes col, col + 16, col + 32, col + 48) summed
 #pragma unroll
-            for (int k = 0; k < 16; ++k) gs1[k] = 0.f;
+            for (int m = 0; m < 4; ++m) {
+                gs1[m] += __shfl_xor(gs1[m], 16);
+                gs1[m] += __shfl_xor(gs1[m], 32);
+            }
+            if (grp == 0)
+                *reinterpret_cast<float4*>(sv + (HEAD == 0 ? DSV_GS1A : DSV_GS1C) + 4 * col) =
+                    make_float4(gs1[0], gs1[1], gs1[2], gs1[3]);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) gs1[m] = 0.f;
         };
         // pass 1's outputs of set j1 and the set vectors pass 2 needs for it
         auto finish1 = [&](int64_t j1) {
@@ -549,7 +474,7 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
                 if (j > 0) finish2(j - 1);
                 else {
 #pragma unroll
-                    for (int k = 0; k < 16; ++k) gs1[k] = 0.f;
+                    for (int m = 0; m < 4; ++m) gs1[m] = 0.f;
                 }
                 if (j < n) finish1(j);
                 reset1();
@@ -565,18 +490,20 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
     }
     // the block's waves summed in LDS in a fixed order, one slot per block
     __syncthreads();
-    float* red = &TB[0][0][0];
+    float* red = &TB[0][0];
     static_assert(sizeof(TB) / sizeof(float) >= DSW_FLOATS, "reduction buffer");
     for (int w = 0; w < DSB_WAVES; ++w) {
         if (wv == w) {
+            // accumulator (mt, nt) reg i of lane (col, grp): output feature 16grp + 4i + mt,
+            // input feature 4col + nt (the W layout's feature order); dLambda1 column col
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const int o = 16 * mt + 4 * grp + i;
+                    const int o = 16 * grp + 4 * i + mt;
 #pragma unroll
                     for (int nt = 0; nt < 4; ++nt) {
-                        float& r = red[o * 64 + 16 * nt + col];
+                        float& r = red[o * 64 + 4 * col + nt];
                         r = w == 0 ? w2[mt][nt][i] : r + w2[mt][nt][i];
                     }
                     if (col < 8) {

@@ -2,7 +2,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 T="timeout -k 10"
-$T 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_fused_train.py tests/test_nn_golden.py > gpurun_out/o_tests.log 2>&1 || { tail -30 gpurun_out/o_tests.log; exit 1; }
+$T 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_fused_train.py tests/test_nn_golden.py tests/test_gpu_learners.py > gpurun_out/o_tests.log 2>&1 || { tail -30 gpurun_out/o_tests.log; exit 1; }
 tail -1 gpurun_out/o_tests.log
 for l in ${LIBS:-bwd_old bwd_il2}; do $T 120 python tools/train_bench.py --lib exp/$l.so > gpurun_out/o_$l.json 2>&1 || exit 1; grep -h sets gpurun_out/o_$l.json; done
 if [ -n "$PMC" ]; then
