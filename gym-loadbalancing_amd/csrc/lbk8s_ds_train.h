@@ -248,11 +248,11 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
         cv[64 + lane] = cv[128 + lane] = cv[192 + lane] = 0.f;
         cvb[1024 + lane] = cvb[1088 + lane] = 0xff;
         // pass-1 state (lane = feature) and pass 2's per-set sums
-        float mx2, mx1, S, G, m0, g3, gs1[4];
+        float mx2, mx1, S, G, S1, G1, m0, g3, gs1[4];
         int r2, r1;
         auto reset1 = [&]() {
             mx2 = mx1 = m0 = -INFINITY;
-            S = G = g3 = 0.f;
+            S = G = S1 = G1 = g3 = 0.f;
             r2 = r1 = 0;
         };
         reset1();
@@ -262,17 +262,24 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
 
         // pass 1 on rows 16t + q0 .. 16t + q0 + 3; wl: the row weights (lane j: row 16t + j),
         // dl (actor) / 1 (critic), 0 past R
-        auto pass1 = [&](int t, const Rows1& c, float wl, int q0) {
+        auto pass1 = [&](int t, const Rows1& c, const float4& w4, int q0) {
 #pragma clang fp contract(fast)
+            const float wq[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
             for (int q = q0; q < q0 + 4; ++q) {
                 const int r = 16 * t + q;
-                const float w = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, wl), q));
+                const float w = wq[q - q0];
                 const bool u2 = c.a[q] > mx2;  // strict: rows ascend, the first maximum stays
                 mx2 = u2 ? c.a[q] : mx2;
                 r2 = u2 ? r : r2;
-                S += w * fminf(c.a[q], 0.f);
-                G += w * c.a[q];  // actor: sum dl h2 (Lambda3); critic: sum c2
+                // two partial sums each (even / odd rows): shorter dependency chains
+                if (q & 1) {
+                    S1 += w * fminf(c.a[q], 0.f);
+                    G1 += w * c.a[q];
+                } else {
+                    S += w * fminf(c.a[q], 0.f);
+                    G += w * c.a[q];  // actor: sum dl h2 (Lambda3); critic: sum c2
+                }
                 const bool u1 = c.h[q] > mx1;
                 mx1 = u1 ? c.h[q] : mx1;
                 r1 = u1 ? r : r1;
@@ -286,6 +293,8 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
             Tile2& c = s.t2;
             const float wl = 16 * t + col < R ? (HEAD == 0 ? s.r1.dl : 1.f) : 0.f;
             if (HEAD == 0) g3 += wl;  // per lane (row 16t + lane & 15); rows summed in finish1
+            // the 16 row weights to every lane through the wave's LDS scratch (float4 reads)
+            if (lane < 16) cv[lane] = wl;
             // Lambda2^T and the set vectors re-read from LDS per step: an opaque offset keeps
             // the compiler from hoisting the loop-invariant reads into registers
             uint32_t wo = 0;
@@ -331,7 +340,7 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
                     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
                         for (int nt = 0; nt < 4; ++nt) w2[mt][nt] = mfma4(av[mt], bv[nt], w2[mt][nt]);
-                pass1(t, s.r1, wl, 4 * cs);
+                pass1(t, s.r1, *reinterpret_cast<const float4*>(cv + 4 * cs), 4 * cs);
             }
             m0 = max2(m0, max2(s.r1.x[0], s.r1.x[1]));
             // dz2 in k layout (lane: row col, features 16q + 4grp .. + 3 at k = 4q ..)
@@ -415,6 +424,8 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
         auto finish1 = [&](int64_t j1) {
             const int64_t env = env_of(j1);
             float* sv = p.setvec + env * DSV_FLOATS;
+            S += S1;
+            G += G1;
             sv[(HEAD == 0 ? DSV_MAX2A : DSV_MAX2C) + lane] = mx2;
             sv[(HEAD == 0 ? DSV_MAX1A : DSV_MAX1C) + lane] = mx1;
             sv[(HEAD == 0 ? DSV_GA3 : DSV_CS2) + lane] = G;
