@@ -673,7 +673,7 @@ int lb_ds_forward(const float* frag, const float* obs, int64_t num_envs, int32_t
         return fail("num_elements must be in [1, 257] (LB_DS_MAX_ELEMENTS_FWD)");
     if (!logits_out && !value_out) return 0;
     DSParams p{obs, frag, logits_out, value_out, num_envs, num_elements, logits_out != nullptr, value_out != nullptr,
-               nullptr, nullptr, nullptr, nullptr, nullptr};
+               nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     ds_forward_launch<0>(p, (hipStream_t)stream);
     return check_launch();
 }
@@ -683,7 +683,8 @@ int lb_ds_q_argmax(const float* frag, const float* obs, int64_t num_envs, int32_
     if (!frag || !obs || !actions_out || num_envs < 1) return fail("frag/obs/actions_out NULL or num_envs < 1");
     if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS_FWD)
         return fail("num_elements must be in [1, 257] (LB_DS_MAX_ELEMENTS_FWD)");
-    DSParams p{obs, frag, q_out, nullptr, num_envs, num_elements, 1, 0, nullptr, nullptr, nullptr, actions_out, masks};
+    DSParams p{obs, frag, q_out, nullptr, num_envs, num_elements, 1, 0, nullptr, nullptr, nullptr, nullptr, actions_out,
+               masks};
     ds_forward_launch<2>(p, (hipStream_t)stream);
     return check_launch();
 }
@@ -707,15 +708,16 @@ int lb_replay_add(int64_t num_envs, int32_t obs_floats, int64_t slots, const int
 }
 
 int lb_ds_train_forward(const float* frag, const float* obs, int64_t num_envs, int32_t num_elements,
-                        float* logits_out, float* psi_mean_out, float* save_actor, float* save_critic, void* stream) {
-    if (!frag || !obs || num_envs < 1) return fail("frag/obs NULL or num_envs < 1");
+                        float* logits_out, float* psi_mean_out, float* save_actor, float* save_critic,
+                        float* setvec_out, void* stream) {
+    if (!frag || !obs || !setvec_out || num_envs < 1) return fail("frag/obs/setvec_out NULL or num_envs < 1");
     if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS)
         return fail("num_elements must be in [1, 80] (LB_DS_MAX_ELEMENTS)");
     if (!logits_out && !psi_mean_out) return 0;
     if ((logits_out && !save_actor) || (psi_mean_out && !save_critic))
         return fail("a head's activation buffer is NULL");
     DSParams p{obs, frag, logits_out, nullptr, num_envs, num_elements, logits_out != nullptr, psi_mean_out != nullptr,
-               save_actor, save_critic, psi_mean_out, nullptr, nullptr};
+               save_actor, save_critic, psi_mean_out, setvec_out, nullptr, nullptr};
     ds_forward_launch<1>(p, (hipStream_t)stream);
     return check_launch();
 }

@@ -40,6 +40,8 @@ struct DSParams {
     float* save_actor;    // [2][B][R][64]: actor h1 (after ReLU), h2 (after ELU)
     float* save_critic;   // [2][B][R][64]: critic c1, c2 (after ELU)
     float* psi_mean;      // [B][64]: critic psi output averaged over the set (rho runs in torch)
+    float* setvec;        // [B][LB_DS_SETVEC_FLOATS]: set-wise maxima of the layer inputs and
+                          // their first argmax rows (LB_DSV_MAX*, LB_DSV_ID*), for the backward
     // greedy action (inference only): actions[b] = first argmax over rows of
     // (masks[b][r] ? logits[b][r] : -1e8) (dqn_deepset.py:134-142); NULL = skip
     int32_t* actions;
@@ -153,6 +155,54 @@ __device__ __forceinline__ void set_max_batched(const float (&h)[P * TS][KS], fl
     }
 }
 
+// training forward: each env's set-wise max of a layer input per feature (mb from
+// set_max_batched) and, with IDS, its FIRST argmax row (torch.max's index: the smallest
+// row holding the max) into setvec; lane col == s stores env s.  KS = 16: feature
+// 16(k >> 2) + 4grp + (k & 3); KS = 2 (the observation): feature 4k + grp.
+template <int TS, int P, int KS, bool IDS>
+__device__ __forceinline__ void store_set_max(const float (&h)[P * TS][KS], const float (&mb)[KS], int col, int grp,
+                                              int R, int64_t env0, int64_t B, float* setvec, int off_max,
+                                              int off_id) {
+    constexpr int KW = KS < 4 ? KS : 4;
+#pragma unroll
+    for (int q = 0; q < KS / KW; ++q) {
+        float M[KW * P], c[KW * P];
+#pragma unroll
+        for (int kk = 0; kk < KW; ++kk)
+#pragma unroll
+            for (int s = 0; s < P; ++s) {
+                const int k = q * KW + kk;
+                M[kk * P + s] = from_col_dyn<P>(mb[k], s);
+                if (IDS) {
+                    // descending tiles: the last hit is the first row; only the last tile can
+                    // hold rows past R
+                    float r = (16 * (TS - 1) + col < R && h[s * TS + TS - 1][k] == M[kk * P + s])
+                                  ? (float)(16 * (TS - 1) + col) : 1e9f;
+#pragma unroll
+                    for (int t = TS - 2; t >= 0; --t) r = h[s * TS + t][k] == M[kk * P + s] ? (float)(16 * t + col) : r;
+                    c[kk * P + s] = -r;
+                }
+            }
+        if (IDS) row_reduce<true>(c);
+#pragma unroll
+        for (int s = 0; s < P; ++s) {
+            if (col != s || env0 + s >= B) continue;
+            float* sv = setvec + (env0 + s) * (int64_t)LB_DS_SETVEC_FLOATS;
+            if (KS == 16) {
+                const int f0 = 16 * q + 4 * grp;
+                *reinterpret_cast<float4*>(sv + off_max + f0) = make_float4(M[s], M[P + s], M[2 * P + s], M[3 * P + s]);
+                if (IDS)
+                    *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(sv + off_id) + f0) =
+                        (uint32_t)(-c[s]) | ((uint32_t)(-c[P + s]) << 8) | ((uint32_t)(-c[2 * P + s]) << 16) |
+                        ((uint32_t)(-c[3 * P + s]) << 24);
+            } else {
+#pragma unroll
+                for (int kk = 0; kk < KW; ++kk) sv[off_max + 4 * kk + grp] = M[kk * P + s];
+            }
+        }
+    }
+}
+
 // out = act(Lambda·h - Gamma·max_set(h)), NT 16-row output tiles (4 for 64 outputs)
 template <int TS, int P, int KS, int ACT>
 __device__ __forceinline__ void eq_layer(const float* L, const float* G, const float (&h)[P * TS][KS],
@@ -236,6 +286,7 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
         }
         float m0[2];
         set_max_batched<TS, P, 2>(h0, m0, col, R);
+        if (TRAIN) store_set_max<TS, P, 2, false>(h0, m0, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX0, 0);
 
         float h1[P * TS][16], m1[16], h2[P * TS][16], m2[16];
         // ---- actor: Eq(8->64) ReLU Eq(64->64) ELU Eq(64->1)
@@ -243,9 +294,11 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
             eq_layer<TS, P, 2, 1>(W + DS_A1L, W + DS_A1G, h0, m0, h1, lane);
             if (TRAIN) store_rows<TS, P>(p.save_actor, h1, env0, p.B, R, col, grp);
             set_max_batched<TS, P, 16>(h1, m1, col, R);
+            if (TRAIN) store_set_max<TS, P, 16, true>(h1, m1, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX1A, LB_DSV_ID1A);
             eq_layer<TS, P, 16, 2>(W + DS_A2L, W + DS_A2G, h1, m1, h2, lane);
             if (TRAIN) store_rows<TS, P>(p.save_actor + p.B * (int64_t)R * 64, h2, env0, p.B, R, col, grp);
             set_max_batched<TS, P, 16>(h2, m2, col, R);
+            if (TRAIN) store_set_max<TS, P, 16, true>(h2, m2, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX2A, LB_DSV_ID2A);
             // layer 3 (64 -> 1) on the VALU: a 16-row output tile would use 1/16 of an MFMA.
             // Lane (col, grp) dots its 16 features with Lambda3 / -Gamma3 (row 0 of the
             // fragments: column 0 of its row group), then the 4 row groups are summed.
@@ -304,9 +357,11 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
         eq_layer<TS, P, 2, 2>(W + DS_C1L, W + DS_C1G, h0, m0, h1, lane);
         if (TRAIN) store_rows<TS, P>(p.save_critic, h1, env0, p.B, R, col, grp);
         set_max_batched<TS, P, 16>(h1, m1, col, R);
+        if (TRAIN) store_set_max<TS, P, 16, true>(h1, m1, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX1C, LB_DSV_ID1C);
         eq_layer<TS, P, 16, 2>(W + DS_C2L, W + DS_C2G, h1, m1, h2, lane);
         if (TRAIN) store_rows<TS, P>(p.save_critic + p.B * (int64_t)R * 64, h2, env0, p.B, R, col, grp);
         set_max_batched<TS, P, 16>(h2, m2, col, R);
+        if (TRAIN) store_set_max<TS, P, 16, true>(h2, m2, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX2C, LB_DSV_ID2C);
         // layer 3 has no activation and only its mean over the set is used, so
         // mean_r(Lambda3 c2[r] - Gamma3 max(c2)) = Lambda3 mean_r(c2) - Gamma3 max(c2): one
         // matrix-vector pair on the batched (column c = env c mod P) operands instead of a

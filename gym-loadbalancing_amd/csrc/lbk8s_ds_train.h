@@ -41,9 +41,9 @@ enum : int {
 };
 // per-set vector block (floats); every 64-wide entry is indexed by input feature
 enum : int {
-    DSV_MAX0 = 0,     // [8]  max over the set of the observation
+    DSV_MAX0 = 0,     // [8]  max over the set of the observation (forward)
     DSV_GA3 = 8,      // actor: sum_r dlogit[r] h2[r]           (Lambda3 gradient)
-    DSV_MAX2A = 72,   //        max_set h2                       (Gamma3)
+    DSV_MAX2A = 72,   //        max_set h2 (forward)             (Gamma3)
     DSV_GS2A = 136,   //        sum_r dz2[r]                     (Gamma2)
     DSV_MAX1A = 200,  //        max_set h1                       (Gamma2)
     DSV_GS1A = 264,   //        sum_r dz1[r]                     (Gamma1)
@@ -52,8 +52,19 @@ enum : int {
     DSV_GS2C = 456,   //         sum_r dz2[r]
     DSV_MAX1C = 520,  //         max_set c1
     DSV_GS1C = 584,   //         sum_r dz1[r]
-    DSV_FLOATS = 648,
+    DSV_ID1A = 648,   // [64] u8: first argmax row of max_set h1 / h2 / c1 / c2 (forward)
+    DSV_ID2A = 664,
+    DSV_ID1C = 680,
+    DSV_ID2C = 696,
+    DSV_VA = 712,     // actor: Gamma2^T sum_r dz2 (layer 1's pooled term, applied by the caller)
+    DSV_VC = 776,     // critic
+    DSV_FLOATS = 840,
 };
+static_assert(DSV_MAX1A == LB_DSV_MAX1A && DSV_MAX2A == LB_DSV_MAX2A && DSV_MAX1C == LB_DSV_MAX1C &&
+                  DSV_MAX2C == LB_DSV_MAX2C && DSV_ID1A == LB_DSV_ID1A && DSV_ID2A == LB_DSV_ID2A &&
+                  DSV_ID1C == LB_DSV_ID1C && DSV_ID2C == LB_DSV_ID2C && DSV_VA == LB_DSV_VA && DSV_VC == LB_DSV_VC &&
+                  DSV_MAX0 == LB_DSV_MAX0,
+              "per-set vector layout and header disagree");
 
 constexpr int DSB_BLOCK = 256;                       // 4 waves: 1 per SIMD, one block per CU
 constexpr int DSW_FLOATS = 4608;                     // per head: dLambda2 [64][64], dLambda1 [64][8]
@@ -84,92 +95,78 @@ __device__ __forceinline__ float dact(float y) {
 // ---- the backward kernel
 //
 // One wave per SIMD (4 per CU, 512 registers each).  A wave walks its sets (env0, env0 +
-// nwaves, ...) as one stream of 16-row steps; step t of iteration j runs
-//   pass 1 (VALU) on rows 16t..16t+15 of set j, transposed: lane f owns feature f and
-//     walks the rows in order, so the set-wise max, its FIRST argmax row (strict > over
-//     ascending rows) and the set sums need no cross-lane reduction;
-//   pass 2 (MFMA) on tile t of set j - 1 (whose set vectors pass 1 finished one iteration
-//     earlier), in the W layout: lane (col, grp) holds rows 4c + grp (c < 4) and features
-//     4col .. 4col + 3, which is the operand layout of dLambda2 += dz2^T h1 and dLambda1 +=
-//     dz1^T obs (contraction over rows), so those MFMAs read registers.  The data gradient
-//     (contraction over features, dz1 = dz2 Lambda2, Lambda2^T from LDS) needs rows in the
-//     other index: dz2 goes through a per-wave LDS transpose into it and dz1 back;
-// in one basic block, with pass 1's quarters between the dLambda2 k-steps, so the vector
-// work issues in the matrix instructions' shadow.  Iteration 0 runs pass 2 on a dummy set
-// with zero set vectors (it adds nothing) and iteration n pass 1 on a dummy whose results
-// are dropped.  Every step loads the next step's rows before it computes (two buffers,
-// used alternately).  Between iterations: pass 2's per-set sums go out (finish2), and
-// pass 1's set vectors (c1, c2, v: below) are built by lane-per-feature matrix-vector
-// products against natural-order weights in LDS (finish1).
+// nwaves, ...) 16 rows at a time.  The set-wise maxima and their first argmax rows come
+// from the training forward (setvec MAX*, ID*), so each set is read once:
+//   per set, before its first tile: the set vectors c1, c2 (below), from the actor's
+//     dlogits (g3 = sum_r dl[r]) or the critic's dmean (lane-per-feature matrix-vector
+//     products against natural-order weights in LDS);
+//   per 16-row tile, in the W layout (lane (col, grp) holds rows 4c + grp, c < 4, and
+//     features 4col .. 4col + 3, which is the operand layout of dLambda2 += dz2^T h1 and
+//     dLambda1 += dz1^T obs, contractions over rows, so those MFMAs read registers):
+//     dz2; dLambda2; the data gradient dz1 = (dz2 Lambda2) act'(h1) (contraction over
+//     features: dz2 goes through a per-wave LDS transpose into the MFMA's other operand
+//     layout and the result back, Lambda2^T from LDS); dLambda1; the set sums S, G of h2
+//     terms and of dz1;
+//   per set, after its last tile: sum_r dz2 in closed form, V = Gamma2^T sum_r dz2, the set
+//     sums out.  Layer 1's pooled term (dz1 at row ID1[o] of feature o carries -V[o]
+//     act'(MAX1[o])) is the caller's (lbk8s.h): it touches one row per feature.
+// Every step loads the next step's tile before it computes (two buffers, used alternately),
+// and each set's small inputs (dlogits or dmean, ID2, MAX2) are loaded one set ahead.
 //
-// Per feature o, dz2[r][o] = (c1[o] - [r == argmax] c2[o]) elu'(h2[r][o]) with actor
-// c1 = dl[r] Lambda3[o] (row-dependent through dl), c2 = g3 Gamma3[o], g3 = sum_r dl[r];
+// Per feature o, dz2[r][o] = (c1[o] - [r == ID2[o]] c2[o]) elu'(h2[r][o]) with actor
+// c1 = dl[r] Lambda3[o] (row-dependent through dl), c2 = g3 Gamma3[o];
 // critic c1 = u[o] = (Lambda3^T dmean)[o] / R, c2 = vv[o] = (Gamma3^T dmean)[o].  Its set
-// sum is closed-form: sum_r dz2[r][o] = c1 S[o] - c2 elu'(max_r h2[r][o]) with
+// sum is closed-form: sum_r dz2[r][o] = c1 S[o] - c2 elu'(MAX2[o]) with
 // S = sum_r w[r] elu'(h2[r][o]) = sum_r w[r] min(h2[r][o], 0) + sum_r w[r] (ELU output y:
 // elu' = y > 0 ? 1 : y + 1 = min(y, 0) + 1), w = dl (actor) / 1 (critic).
 constexpr int DSB_WAVES = DSB_BLOCK / 64;
 constexpr int DSB_NAT = 3 * 4096 + 128;  // natural-order weights (below)
-constexpr int DSB_CV = 384;              // per-wave set vectors (below)
+constexpr int DSB_CV = 192;              // per-wave set vectors (below)
 
-// pass-2 input tile as loaded: rows past R read row R - 1 (finite values, in bounds) and
-// every use masks them, so no instruction touches the registers before the tile is used
-// W layout (the weight-gradient MFMAs' operand layout): lane (col, grp) holds, for each
-// 4-row group c, row 16t + 4c + grp and features 4col .. 4col + 3 (one float4)
+// one 16-row tile of the backward's inputs in the W layout, as loaded: rows past R read
+// row R - 1 (finite values, in bounds) and every use masks them, so no instruction touches
+// the registers before the tile is used
 struct Tile2 {
-    float4 a[4];  // h2 / c2
+    float4 a[4];  // h2 / c2 of row 16t + 4c + grp, features 4col .. 4col + 3
     float4 h[4];  // h1 / c1
     float x[4];   // observation feature col & 7 of row 16t + 4c + grp
     float d[4];   // the actor's dlogit of row 16t + 4c + grp
 };
-// pass-1 rows 16t + q (q < 16), lane = feature; rows past R repeat row R - 1 (a repeated
-// row changes no max / first argmax, and gets weight 0 in the sums)
-struct Rows1 {
-    float a[16], h[16];  // h2 / c2, h1 / c1 of feature lane
-    float x[2];          // observation feature lane & 7 of rows 16t + (lane >> 3), + 8
-    float dl;            // the actor's dlogit of row 16t + (lane & 15)
-};
-struct StepIn {
-    Tile2 t2;
-    Rows1 r1;
+// a set's small inputs, loaded one set ahead
+struct SetIn {
+    float dl0, dl1;  // actor: dlogits of rows lane, lane + 64 (0 past R)
+    float dm;        // critic: dmean[lane]
+    int id2;         // ID2 bytes of features 4col .. 4col + 3
+    float4 mx2;      // MAX2 of features 4col .. 4col + 3
 };
 
 template <int HEAD>
-__device__ __forceinline__ void load_step(const DSBwdParams& p, const float* in1, const float* in2, int64_t env2,
-                                          int64_t env1, int t, int lane, StepIn& s) {
-    const int R = p.R, col = lane & 15, grp = lane >> 4;
+__device__ __forceinline__ void load_tile2(const DSBwdParams& p, const float* in1, const float* in2, int64_t env, int t,
+                                           int col, int grp, Tile2& s) {
+    const int R = p.R;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        const int64_t er = env2 * (int64_t)R + min(16 * t + 4 * c + grp, R - 1);
-        s.t2.a[c] = *reinterpret_cast<const float4*>(in2 + er * 64 + 4 * col);
-        s.t2.h[c] = *reinterpret_cast<const float4*>(in1 + er * 64 + 4 * col);
-        s.t2.x[c] = p.obs[er * 8 + (col & 7)];
-        s.t2.d[c] = HEAD == 0 ? p.dlogits[er] : 0.f;
+        const int64_t er = env * (int64_t)R + min(16 * t + 4 * c + grp, R - 1);
+        s.a[c] = *reinterpret_cast<const float4*>(in2 + er * 64 + 4 * col);
+        s.h[c] = *reinterpret_cast<const float4*>(in1 + er * 64 + 4 * col);
+        s.x[c] = p.obs[er * 8 + (col & 7)];
+        s.d[c] = HEAD == 0 ? p.dlogits[er] : 0.f;
     }
-    {
-        // one wave-uniform base per plane, the rows at immediate offsets
-        const int64_t e0 = env1 * (int64_t)R, rb = e0 + 16 * t;
-        const float* b2 = in2 + rb * 64 + lane;
-        const float* b1 = in1 + rb * 64 + lane;
-        if (16 * t + 16 <= R) {
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                s.r1.a[q] = b2[q * 64];
-                s.r1.h[q] = b1[q * 64];
-            }
-        } else {
-            const int qmax = R - 1 - 16 * t;
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int qq = min(q, qmax);
-                s.r1.a[q] = b2[qq * 64];
-                s.r1.h[q] = b1[qq * 64];
-            }
-        }
-        s.r1.x[0] = p.obs[(e0 + min(16 * t + (lane >> 3), R - 1)) * 8 + (lane & 7)];
-        s.r1.x[1] = p.obs[(e0 + min(16 * t + 8 + (lane >> 3), R - 1)) * 8 + (lane & 7)];
-        s.r1.dl = HEAD == 0 ? p.dlogits[e0 + min(16 * t + col, R - 1)] : 0.f;
+}
+
+template <int HEAD>
+__device__ __forceinline__ void load_setin(const DSBwdParams& p, int64_t env, int lane, int col, SetIn& s) {
+    const int R = p.R;
+    const float* sv = p.setvec + env * (int64_t)DSV_FLOATS;
+    if (HEAD == 0) {
+        const float* dl = p.dlogits + env * (int64_t)R;
+        s.dl0 = lane < R ? dl[lane] : 0.f;
+        s.dl1 = lane + 64 < R ? dl[lane + 64] : 0.f;
+    } else {
+        s.dm = p.dmean[env * 64 + lane];
     }
+    s.id2 = *reinterpret_cast<const int*>(reinterpret_cast<const uint8_t*>(sv + (HEAD == 0 ? DSV_ID2A : DSV_ID2C)) + 4 * col);
+    s.mx2 = *reinterpret_cast<const float4*>(sv + (HEAD == 0 ? DSV_MAX2A : DSV_MAX2C) + 4 * col);
 }
 
 // lane-per-feature matrix-vector product out[lane] = sum_i M[i][lane] x[i], M natural
@@ -187,21 +184,20 @@ __device__ __forceinline__ float matvec64(const float* M, const float* x, int la
     return acc;
 }
 
-// One launch per head (HEAD 0 actor, 1 critic).
-// NCT: 4-row groups of the last tile that hold set rows (ceil(((R - 1) % 16 + 1) / 4)); the
-// last tile's weight-gradient products skip the groups past R.
+// One launch per head (HEAD 0 actor, 1 critic).  NCT: 4-row groups of the last tile that
+// hold set rows (ceil(((R - 1) % 16 + 1) / 4)); the last tile's weight-gradient products
+// skip the groups past R.
 template <int HEAD, int NCT>
 __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
     constexpr int ACT1 = HEAD == 0 ? 1 : 2;  // activation after layer 1: ReLU (actor) / ELU (critic)
     // natural-order weights [i][o] (W[out i][in o]): Gamma2 at 0; the critic's Lambda3,
     // Gamma3 at 4096, 8192; the actor's Lambda3 / Gamma3 rows at 12288 / 12352
     __shared__ __attribute__((aligned(16))) float NAT[DSB_NAT];
-    // Lambda2^T in fragment order (the eq-back's A operands)
+    // Lambda2^T in fragment order (the data gradient's A operands)
     __shared__ __attribute__((aligned(16))) float LT[4096];
     // per wave: the 16-row tile transposes (16 x 16 float4), and the block's reduction
     __shared__ __attribute__((aligned(16))) float TB[DSB_WAVES][DST_FLOATS];
-    // per wave: [0,64) broadcast scratch, c1 [64,128), c2 [128,192), v [192,256), argmax
-    // rows as bytes (id2 at byte 1024 + f, id1 at 1088 + f)
+    // per wave: [0, 64) broadcast scratch, c1 [64, 128), c2 [128, 192) of the current set
     __shared__ __attribute__((aligned(16))) float CV[DSB_WAVES][DSB_CV];
     {
         // fragment image -> natural order: fragment (nt, k), lane l holds W^T[o][i] with
@@ -227,13 +223,11 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
     const int64_t nwaves = (int64_t)gridDim.x * DSB_WAVES;
     float* la = TB[wv];
     float* cv = CV[wv];
-    uint8_t* cvb = reinterpret_cast<uint8_t*>(cv);
     const int R = p.R, ntl = (R + 15) / 16;
     const int col = lane & 15, grp = lane >> 4;
     const int64_t plane = p.B * (int64_t)R * 64;
     const float* in1 = HEAD == 0 ? p.save_actor : p.save_critic;  // h1 / c1
     const float* in2 = in1 + plane;                                 // h2 / c2
-    const bool do_max0 = HEAD == 0 || !p.actor;
     dsf4 w2[4][4], w1[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
@@ -244,105 +238,122 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
     const int64_t env0 = (int64_t)blockIdx.x * DSB_WAVES + wv;
     const int64_t n = env0 < p.B ? (p.B - 1 - env0) / nwaves + 1 : 0;  // this wave's sets
     if (n > 0) {
-        // set vectors of the set pass 2 works on (zero for the dummy, no argmax row)
-        cv[64 + lane] = cv[128 + lane] = cv[192 + lane] = 0.f;
-        cvb[1024 + lane] = cvb[1088 + lane] = 0xff;
-        // pass-1 state (lane = feature) and pass 2's per-set sums
-        float mx2, mx1, S, G, S1, G1, m0, g3, gs1[4];
-        int r2, r1;
-        auto reset1 = [&]() {
-            mx2 = mx1 = m0 = -INFINITY;
-            S = G = S1 = G1 = g3 = 0.f;
-            r2 = r1 = 0;
-        };
-        reset1();
-#pragma unroll
-        for (int m = 0; m < 4; ++m) gs1[m] = 0.f;
         auto env_of = [&](int64_t j) { return env0 + j * nwaves; };
-
-        // pass 1 on rows 16t + q0 .. 16t + q0 + 3; wl: the row weights (lane j: row 16t + j),
-        // dl (actor) / 1 (critic), 0 past R
-        auto pass1 = [&](int t, const Rows1& c, const float4& w4, int q0) {
-#pragma clang fp contract(fast)
-            const float wq[4] = {w4.x, w4.y, w4.z, w4.w};
+        // per-set state (W layout: this lane's rows, features 4col .. 4col + 3)
+        float S4[4], G4[4], gs1[4], g3 = 0.f;
+        int id2w = 0;
+        float4 mx2v;
 #pragma unroll
-            for (int q = q0; q < q0 + 4; ++q) {
-                const int r = 16 * t + q;
-                const float w = wq[q - q0];
-                const bool u2 = c.a[q] > mx2;  // strict: rows ascend, the first maximum stays
-                mx2 = u2 ? c.a[q] : mx2;
-                r2 = u2 ? r : r2;
-                // two partial sums each (even / odd rows): shorter dependency chains
-                if (q & 1) {
-                    S1 += w * fminf(c.a[q], 0.f);
-                    G1 += w * c.a[q];
-                } else {
-                    S += w * fminf(c.a[q], 0.f);
-                    G += w * c.a[q];  // actor: sum dl h2 (Lambda3); critic: sum c2
-                }
-                const bool u1 = c.h[q] > mx1;
-                mx1 = u1 ? c.h[q] : mx1;
-                r1 = u1 ? r : r1;
+        for (int m = 0; m < 4; ++m) S4[m] = G4[m] = gs1[m] = 0.f;
+        SetIn pre;
+        load_setin<HEAD>(p, env_of(0), lane, col, pre);
+
+        // the set vectors of set j (c1, c2 to LDS), then set j + 1's inputs requested
+        auto prologue = [&](int64_t j) {
+            const SetIn cur = pre;
+            if (j + 1 < n) load_setin<HEAD>(p, env_of(j + 1), lane, col, pre);
+            id2w = cur.id2;
+            mx2v = cur.mx2;
+            float c1, c2;
+            if (HEAD == 0) {
+                float s = cur.dl0 + cur.dl1;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+                g3 = s;
+                c1 = NAT[12288 + lane];
+                c2 = g3 * NAT[12352 + lane];
+            } else {
+                cv[lane] = cur.dm;
+                c1 = matvec64(NAT + 4096, cv, lane, 1.0f / (float)R);
+                c2 = matvec64(NAT + 8192, cv, lane);
             }
+            cv[64 + lane] = c1;
+            cv[128 + lane] = c2;
         };
-        // one step's work: pass 2 on tile t of the older set, pass 1 on rows 16t.. of the
-        // newer, pass 1's quarters placed between the weight-gradient MFMA groups
-        auto compute = [&](int t, StepIn& s, auto ncc) {
+        // the set sums of set j out, V = Gamma2^T sum_r dz2
+        auto epilogue = [&](int64_t j) {
+            float* sv = p.setvec + env_of(j) * (int64_t)DSV_FLOATS;
+            // the four row groups (lanes col, col + 16, col + 32, col + 48) summed
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                S4[m] += __shfl_xor(S4[m], 16);
+                S4[m] += __shfl_xor(S4[m], 32);
+                G4[m] += __shfl_xor(G4[m], 16);
+                G4[m] += __shfl_xor(G4[m], 32);
+                gs1[m] += __shfl_xor(gs1[m], 16);
+                gs1[m] += __shfl_xor(gs1[m], 32);
+            }
+            const float4 c1v = *reinterpret_cast<const float4*>(cv + 64 + 4 * col);
+            const float4 c2v = *reinterpret_cast<const float4*>(cv + 128 + 4 * col);
+            const float c1a[4] = {c1v.x, c1v.y, c1v.z, c1v.w}, c2a[4] = {c2v.x, c2v.y, c2v.z, c2v.w};
+            const float ma[4] = {mx2v.x, mx2v.y, mx2v.z, mx2v.w};
+            const float wsum = HEAD == 0 ? g3 : (float)R;
+            float gs[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) gs[m] = c1a[m] * (S4[m] + wsum) - c2a[m] * dact<2>(ma[m]);
+            if (grp == 0) {
+                *reinterpret_cast<float4*>(sv + (HEAD == 0 ? DSV_GS2A : DSV_GS2C) + 4 * col) =
+                    make_float4(gs[0], gs[1], gs[2], gs[3]);
+                *reinterpret_cast<float4*>(sv + (HEAD == 0 ? DSV_GA3 : DSV_CS2) + 4 * col) =
+                    make_float4(G4[0], G4[1], G4[2], G4[3]);
+                *reinterpret_cast<float4*>(sv + (HEAD == 0 ? DSV_GS1A : DSV_GS1C) + 4 * col) =
+                    make_float4(gs1[0], gs1[1], gs1[2], gs1[3]);
+                *reinterpret_cast<float4*>(cv + 4 * col) = make_float4(gs[0], gs[1], gs[2], gs[3]);
+            }
+            sv[(HEAD == 0 ? DSV_VA : DSV_VC) + lane] = matvec64(NAT, cv, lane);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) S4[m] = G4[m] = gs1[m] = 0.f;
+        };
+        // one 16-row tile of the current set
+        auto compute = [&](int t, Tile2& c, auto ncc) {
 #pragma clang fp contract(fast)
             constexpr int NC = decltype(ncc)::value;  // 4-row groups with set rows
-            Tile2& c = s.t2;
-            const float wl = 16 * t + col < R ? (HEAD == 0 ? s.r1.dl : 1.f) : 0.f;
-            if (HEAD == 0) g3 += wl;  // per lane (row 16t + lane & 15); rows summed in finish1
-            // the 16 row weights to every lane through the wave's LDS scratch (float4 reads)
-            if (lane < 16) cv[lane] = wl;
-            // Lambda2^T and the set vectors re-read from LDS per step: an opaque offset keeps
+            // Lambda2^T and the set vectors re-read from LDS per tile: an opaque offset keeps
             // the compiler from hoisting the loop-invariant reads into registers
             uint32_t wo = 0;
             asm volatile("" : "+s"(wo));
             const float* LTt = LT + wo;
             const float* cvt = cv + wo;
-            // set vectors of features 4col .. 4col + 3 (W layout)
             const float4 c1v = *reinterpret_cast<const float4*>(cvt + 64 + 4 * col);
             const float4 c2v = *reinterpret_cast<const float4*>(cvt + 128 + 4 * col);
-            const int id2w = *reinterpret_cast<const int*>(reinterpret_cast<const uint8_t*>(cvt) + 1024 + 4 * col);
-            // dz2 = (w c1 - [r == argmax] c2) elu'(h2), elu' = min(y, 0) + 1; rows past R have
-            // w = 0 and are never an argmax, so their dz2 (and dz1) is 0
+            // dz2 = (w c1 - [r == ID2] c2) elu'(h2); rows past R have w = 0 and are never an
+            // argmax, so their dz2 (and dz1) is 0; the set sums S, G of the h2 terms
             float4 dz[4];
 #pragma unroll
             for (int cc = 0; cc < 4; ++cc) {
                 const int row = 16 * t + 4 * cc + grp;
                 const float w = row < R ? (HEAD == 0 ? c.d[cc] : 1.f) : 0.f;
-                float x[4], y[4] = {c.a[cc].x, c.a[cc].y, c.a[cc].z, c.a[cc].w};
+                float x[4];
+                const float y[4] = {c.a[cc].x, c.a[cc].y, c.a[cc].z, c.a[cc].w};
                 const float c1a[4] = {c1v.x, c1v.y, c1v.z, c1v.w}, c2a[4] = {c2v.x, c2v.y, c2v.z, c2v.w};
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
+                    const float mn = fminf(y[m], 0.f);
                     const float u = w * c1a[m] - (row == ((id2w >> (8 * m)) & 0xff) ? c2a[m] : 0.f);
-                    x[m] = u * fminf(y[m], 0.f) + u;
+                    x[m] = u * mn + u;
+                    S4[m] += w * mn;
+                    G4[m] += w * y[m];  // actor: sum dl h2 (Lambda3); critic: sum c2
                 }
                 dz[cc] = make_float4(x[0], x[1], x[2], x[3]);
             }
-            // the tile through LDS into the eq-back's k layout (row = col): float4 q of row rho
-            // at rho * 16 + (q ^ rho), conflict-free both ways
+            // the tile through LDS into the data gradient's k layout (row = col): float4 q of
+            // row rho at rho * 16 + (q ^ rho), conflict-free both ways
             float4* T4 = reinterpret_cast<float4*>(la);
 #pragma unroll
             for (int cc = 0; cc < 4; ++cc) {
                 const int rho = 4 * cc + grp;
                 T4[rho * 16 + (col ^ rho)] = dz[cc];
             }
-            // dLambda2 += dz2^T h1 straight from registers (W layout = the MFMA operands),
-            // k-step by k-step, a pass-1 quarter after each
+            // dLambda2 += dz2^T h1 straight from registers (W layout = the MFMA operands)
 #pragma unroll
-            for (int cs = 0; cs < 4; ++cs) {
+            for (int cs = 0; cs < NC; ++cs) {
                 const float av[4] = {dz[cs].x, dz[cs].y, dz[cs].z, dz[cs].w};
                 const float bv[4] = {c.h[cs].x, c.h[cs].y, c.h[cs].z, c.h[cs].w};
-                if (cs < NC)
 #pragma unroll
-                    for (int mt = 0; mt < 4; ++mt)
+                for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-                        for (int nt = 0; nt < 4; ++nt) w2[mt][nt] = mfma4(av[mt], bv[nt], w2[mt][nt]);
-                pass1(t, s.r1, *reinterpret_cast<const float4*>(cv + 4 * cs), 4 * cs);
+                    for (int nt = 0; nt < 4; ++nt) w2[mt][nt] = mfma4(av[mt], bv[nt], w2[mt][nt]);
             }
-            m0 = max2(m0, max2(s.r1.x[0], s.r1.x[1]));
             // dz2 in k layout (lane: row col, features 16q + 4grp .. + 3 at k = 4q ..)
             float dk[16];
 #pragma unroll
@@ -380,22 +391,18 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt)
                 T4[col * 16 + ((4 * nt + grp) ^ col)] = make_float4(eacc[nt][0], eacc[nt][1], eacc[nt][2], eacc[nt][3]);
-            const float4 vv = *reinterpret_cast<const float4*>(cvt + 192 + 4 * col);
-            const int id1w = *reinterpret_cast<const int*>(reinterpret_cast<const uint8_t*>(cvt) + 1088 + 4 * col);
-            const float va[4] = {vv.x, vv.y, vv.z, vv.w};
-            // dz1 = (pre - [r == argmax] Gamma2^T sum dz2) act'(h1), W layout; its set sum;
+            // dz1 = pre act'(h1) (W layout; the pooled term is the caller's), its set sum,
             // dLambda1 += dz1^T obs (B columns 8..15 zero)
 #pragma unroll
             for (int cc = 0; cc < 4; ++cc) {
-                const int rho = 4 * cc + grp, row = 16 * t + rho;
+                const int rho = 4 * cc + grp;
                 const float4 pre = T4[rho * 16 + (col ^ rho)];
                 const float pa[4] = {pre.x, pre.y, pre.z, pre.w};
                 const float ha[4] = {c.h[cc].x, c.h[cc].y, c.h[cc].z, c.h[cc].w};
                 float d1[4];
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
-                    const float u = pa[m] - (row == ((id1w >> (8 * m)) & 0xff) ? va[m] : 0.f);
-                    d1[m] = ACT1 == 1 ? (ha[m] > 0.f ? u : 0.f) : u * fminf(ha[m], 0.f) + u;
+                    d1[m] = ACT1 == 1 ? (ha[m] > 0.f ? pa[m] : 0.f) : pa[m] * fminf(ha[m], 0.f) + pa[m];
                     gs1[m] += d1[m];
                 }
                 if (cc < NC) {
@@ -405,91 +412,27 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
                 }
             }
         };
-        // pass 2's per-set sums of set j2
-        auto finish2 = [&](int64_t j2) {
-            float* sv = p.setvec + env_of(j2) * DSV_FLOATS;
-            // the four row groups (lanes col, col + 16, col + 32, col + 48) summed
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                gs1[m] += __shfl_xor(gs1[m], 16);
-                gs1[m] += __shfl_xor(gs1[m], 32);
-            }
-            if (grp == 0)
-                *reinterpret_cast<float4*>(sv + (HEAD == 0 ? DSV_GS1A : DSV_GS1C) + 4 * col) =
-                    make_float4(gs1[0], gs1[1], gs1[2], gs1[3]);
-#pragma unroll
-            for (int m = 0; m < 4; ++m) gs1[m] = 0.f;
-        };
-        // pass 1's outputs of set j1 and the set vectors pass 2 needs for it
-        auto finish1 = [&](int64_t j1) {
-            const int64_t env = env_of(j1);
-            float* sv = p.setvec + env * DSV_FLOATS;
-            S += S1;
-            G += G1;
-            sv[(HEAD == 0 ? DSV_MAX2A : DSV_MAX2C) + lane] = mx2;
-            sv[(HEAD == 0 ? DSV_MAX1A : DSV_MAX1C) + lane] = mx1;
-            sv[(HEAD == 0 ? DSV_GA3 : DSV_CS2) + lane] = G;
-            if (do_max0) {
-                // lanes with equal (lane & 7) hold the same observation feature
-                m0 = max2(m0, __shfl_xor(m0, 8));
-                m0 = max2(m0, __shfl_xor(m0, 16));
-                m0 = max2(m0, __shfl_xor(m0, 32));
-                if (lane < 8) sv[DSV_MAX0 + lane] = m0;
-            }
-            float c1, c2;
-            if (HEAD == 0) {
-                // g3 = sum of the set's dlogits: per lane over its rows, then over 16 lanes
-                float gv[4] = {g3, 0.f, 0.f, 0.f};
-                row_reduce<false>(gv);
-                g3 = gv[0];
-                S += g3;
-                c1 = NAT[12288 + lane];
-                c2 = g3 * NAT[12352 + lane];
-            } else {
-                S += (float)R;
-                cv[lane] = p.dmean[env * 64 + lane];
-                c1 = matvec64(NAT + 4096, cv, lane, 1.0f / (float)R);
-                c2 = matvec64(NAT + 8192, cv, lane);
-            }
-            const float gs = c1 * S - c2 * dact<2>(mx2);
-            sv[(HEAD == 0 ? DSV_GS2A : DSV_GS2C) + lane] = gs;
-            cv[64 + lane] = c1;
-            cv[128 + lane] = c2;
-            cvb[1024 + lane] = (uint8_t)r2;
-            cvb[1088 + lane] = (uint8_t)r1;
-            cv[lane] = gs;
-            cv[192 + lane] = matvec64(NAT, cv, lane);  // v = Gamma2^T (sum dz2)
-        };
 
-        // step g = j * ntl + t of the stream, j in [0, n]: pass 1 on set min(j, n - 1),
-        // pass 2 on set max(j - 1, 0)
-        const int64_t steps = (n + 1) * ntl;
+        // the stream of tiles g = j * ntl + t, j < n; two tile buffers used alternately
+        const int64_t steps = n * ntl;
         int64_t j = 0;
         int t = 0;
-        StepIn A, B;
-        load_step<HEAD>(p, in1, in2, env_of(0), env_of(0), 0, lane, A);
-        auto step = [&](StepIn& cur, StepIn& nxt, bool more) {
+        Tile2 A, B;
+        load_tile2<HEAD>(p, in1, in2, env_of(0), 0, col, grp, A);
+        auto step = [&](Tile2& cur, Tile2& nxt, bool more) {
             int tn = t + 1;
             int64_t jn = j;
             if (tn == ntl) {
                 tn = 0;
                 ++jn;
             }
-            if (more)
-                load_step<HEAD>(p, in1, in2, env_of(jn > 0 ? jn - 1 : 0), env_of(jn < n ? jn : n - 1), tn, lane, nxt);
+            if (t == 0) prologue(j);
+            if (more) load_tile2<HEAD>(p, in1, in2, env_of(jn), tn, col, grp, nxt);
             if (NCT < 4 && t == ntl - 1)
                 compute(t, cur, std::integral_constant<int, NCT>{});
             else
                 compute(t, cur, std::integral_constant<int, 4>{});
-            if (tn == 0) {
-                if (j > 0) finish2(j - 1);
-                else {
-#pragma unroll
-                    for (int m = 0; m < 4; ++m) gs1[m] = 0.f;
-                }
-                if (j < n) finish1(j);
-                reset1();
-            }
+            if (tn == 0) epilogue(j);
             t = tn;
             j = jn;
         };

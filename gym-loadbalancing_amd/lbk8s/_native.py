@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblbk8s.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 LB_REWARD = {"naive": 0, "latency": 1, "fairness": 2, "multi": 3}
 LB_RNG_PHILOX, LB_RNG_TRACE = 0, 1
@@ -56,11 +56,12 @@ LB_DS_FRAG_FLOATS = 33860
 LB_DS_MAX_ELEMENTS = 80       # training kernels
 LB_DS_MAX_ELEMENTS_FWD = 257  # inference forward / greedy argmax
 LB_DS_BWD_FLOATS = 24704
-LB_DS_SETVEC_FLOATS = 648
+LB_DS_SETVEC_FLOATS = 840
 LB_DS_WGRAD_FLOATS = 4608
 LB_DS_WORKSPACE_FLOATS = 1024 * 2 * LB_DS_WGRAD_FLOATS
 LB_DSV = {"MAX0": 0, "GA3": 8, "MAX2A": 72, "GS2A": 136, "MAX1A": 200, "GS1A": 264, "CS2": 328,
-          "MAX2C": 392, "GS2C": 456, "MAX1C": 520, "GS1C": 584}
+          "MAX2C": 392, "GS2C": 456, "MAX1C": 520, "GS1C": 584, "ID1A": 648, "ID2A": 664, "ID1C": 680,
+          "ID2C": 696, "VA": 712, "VC": 776}
 
 _lib = None
 
@@ -101,7 +102,7 @@ def lib():
     f32 = C.c_float
     L.lb_ppo_head.argtypes = [vp] * 8 + [i64, i32, f32, f32, f32, i32, vp, vp, vp, vp]
     L.lb_replay_add.argtypes = [i64, i32, i64] + [vp] * 15 + [vp]
-    L.lb_ds_train_forward.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp]
+    L.lb_ds_train_forward.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp, vp]
     L.lb_ds_pack_backward.argtypes = [C.POINTER(LBDSWeightsC), vp, vp]
     L.lb_ds_train_backward.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp]
     for f in ("lb_validate_config", "lb_state_bytes", "lb_init", "lb_reset", "lb_step", "lb_policy", "lb_rollout",

@@ -17,7 +17,11 @@ sets — runs in torch:
     critic dLambda3 = (dmean / R)^T sum_r c2[r]          dGamma3 = -dmean^T max_set(c2)
 
 The pooled gradient goes to the first row attaining the max, like torch.max in the
-reference's autograd.  Covered geometry: 8 input features, 64 hidden, 1 <= R <= 80, on a
+reference's autograd.  The forward kernel records each layer input's set-wise max and that
+row (ID1, ID2); layer 1's pooled term touches one row per feature (dz1[ID1[o]][o] carries
+-V[o] act'(MAX1[o]), V = Gamma2^T sum_r dz2 from the backward) and is added here:
+
+    GS1 -= V act'(MAX1)        dLambda1 -= sum_sets (V act'(MAX1))^T obs[ID1]  Covered geometry: 8 input features, 64 hidden, 1 <= R <= 80, on a
 HIP device; `supported()` says whether an input qualifies.
 """
 import ctypes as C
@@ -83,6 +87,22 @@ def _over_sets(a, b):
     return out
 
 
+def _ids(setvec, name):
+    """The u8 argmax rows of a setvec field, as int64 (B, 64)."""
+    o = 4 * DSV[name]
+    return setvec.view(torch.uint8)[:, o:o + 64].long()
+
+
+def _pooled1(x, setvec, dl1, head, relu):
+    """Layer 1's pooled term for one head: (dLambda1, per-set sum of dz1) with the term of
+    the argmax row added (dz1[ID1[o]][o] -= V[o] act'(MAX1[o]))."""
+    mx1 = _vec(setvec, "MAX1" + head)
+    dact = (mx1 > 0).float() if relu else torch.where(mx1 > 0, torch.ones_like(mx1), mx1 + 1)
+    corr = _vec(setvec, "V" + head) * dact                                          # (B, 64)
+    xa = torch.gather(x, 1, _ids(setvec, "ID1" + head).unsqueeze(-1).expand(-1, -1, x.shape[2]))  # (B, 64, 8)
+    return dl1 - (corr.unsqueeze(-1) * xa).sum(0), _vec(setvec, "GS1" + head) - corr
+
+
 class _FusedDeepSetsTrain(torch.autograd.Function):
     """(x, *params) -> (logits (B, R), psi_mean (B, 64) or None).
 
@@ -97,22 +117,23 @@ class _FusedDeepSetsTrain(torch.autograd.Function):
         frag = fused.packed(owner, actor_net, critic)
         logits = torch.empty((B, R), dtype=torch.float32, device=dev)
         save_a = torch.empty((2, B, R, 64), dtype=torch.float32, device=dev)
+        setvec = torch.empty((B, SV), dtype=torch.float32, device=dev)
         mean = save_c = None
         if critic is not None:
             mean = torch.empty((B, 64), dtype=torch.float32, device=dev)
             save_c = torch.empty((2, B, R, 64), dtype=torch.float32, device=dev)
         _native.check(_native.lib().lb_ds_train_forward(
             frag.data_ptr(), x.data_ptr(), B, R, logits.data_ptr(), fused._ptr(mean), save_a.data_ptr(),
-            fused._ptr(save_c), _stream(dev)))
+            fused._ptr(save_c), setvec.data_ptr(), _stream(dev)))
         ctx.actor_net, ctx.critic = actor_net, critic
-        ctx.save_for_backward(x, save_a, save_c)
+        ctx.save_for_backward(x, save_a, save_c, setvec)
         if critic is None:
             return logits
         return logits, mean
 
     @staticmethod
     def backward(ctx, dlogits, dmean=None):
-        x, save_a, save_c = ctx.saved_tensors
+        x, save_a, save_c, setvec = ctx.saved_tensors
         actor_net, critic = ctx.actor_net, ctx.critic
         dev = x.device
         B, R, _ = x.shape
@@ -124,24 +145,25 @@ class _FusedDeepSetsTrain(torch.autograd.Function):
         bfrag = _pack_backward(actor_net, critic, dev)
         wgrad = torch.empty((2, _native.LB_DS_WGRAD_FLOATS), dtype=torch.float32, device=dev)
         work = _workspace(dev)
-        setvec = torch.empty((B, SV), dtype=torch.float32, device=dev)
         _native.check(_native.lib().lb_ds_train_backward(
             bfrag.data_ptr(), x.data_ptr(), B, R, save_a.data_ptr(), fused._ptr(save_c), dlogits.data_ptr(),
             fused._ptr(dmean), wgrad.data_ptr(), work.data_ptr(), setvec.data_ptr(), _stream(dev)))
         max0 = _vec(setvec, "MAX0", 8)
         g3 = dlogits.sum(1)
+        dl1a, gs1a = _pooled1(x, setvec, wgrad[0, 4096:].view(64, 8), "A", relu=True)
         grads = [
-            wgrad[0, 4096:].view(64, 8),                                       # actor Lambda1
-            -_over_sets(_vec(setvec, "GS1A"), max0),                           # actor Gamma1
+            dl1a,                                                              # actor Lambda1
+            -_over_sets(gs1a, max0),                                           # actor Gamma1
             wgrad[0, :4096].view(64, 64),                                      # actor Lambda2
             -_over_sets(_vec(setvec, "GS2A"), _vec(setvec, "MAX1A")),          # actor Gamma2
             _vec(setvec, "GA3").sum(0, keepdim=True),                          # actor Lambda3
             -_over_sets(g3[:, None], _vec(setvec, "MAX2A")),                   # actor Gamma3
         ]
         if critic is not None:
+            dl1c, gs1c = _pooled1(x, setvec, wgrad[1, 4096:].view(64, 8), "C", relu=False)
             grads += [
-                wgrad[1, 4096:].view(64, 8),                                   # critic Lambda1
-                -_over_sets(_vec(setvec, "GS1C"), max0),                       # critic Gamma1
+                dl1c,                                                          # critic Lambda1
+                -_over_sets(gs1c, max0),                                       # critic Gamma1
                 wgrad[1, :4096].view(64, 64),                                  # critic Lambda2
                 -_over_sets(_vec(setvec, "GS2C"), _vec(setvec, "MAX1C")),      # critic Gamma2
                 _over_sets(dmean / R, _vec(setvec, "CS2")),                    # critic Lambda3

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LBK8S_ABI_VERSION 3
+#define LBK8S_ABI_VERSION 4
 
 /* reward_function names of loadbalancer_k8s_env.py:20-31 */
 enum { LB_REWARD_NAIVE = 0, LB_REWARD_LATENCY = 1, LB_REWARD_FAIRNESS = 2, LB_REWARD_MULTI = 3 };
@@ -243,17 +243,21 @@ int lb_replay_add(int64_t num_envs, int32_t obs_floats, int64_t slots, const int
 /* ---- Fused deep-sets training -----------------------------
  * Replaces the reference's autograd through the same modules in the PPO update
  * (envs/ppo_deepset.py:227-263 -> deep_sets_agent_original.py:56-106).  The training
- * step is split: lb_ds_train_forward (logits, the critic's psi mean before rho, and the
- * hidden activations), the loss and rho in the caller (torch), lb_ds_train_backward (each
- * head's dLambda2 = dz2^T h1 and dLambda1 = dz1^T obs, accumulated in the kernel, plus
- * per-set vectors), then the remaining weight gradients as small GEMMs over the sets
- * (the caller; lbk8s/fused_train.py spells them out):
+ * step is split: lb_ds_train_forward (logits, the critic's psi mean before rho, the hidden
+ * activations, and per set the layer inputs' set-wise maxima with their first argmax rows),
+ * the loss and rho in the caller (torch), lb_ds_train_backward (each head's dLambda2 =
+ * dz2^T h1 and dLambda1 = dz1^T obs, accumulated in the kernel, plus per-set vectors), then
+ * the remaining weight gradients as small GEMMs over the sets (the caller;
+ * lbk8s/fused_train.py spells them out):
  *   dGamma_l = -(per-set sum of dz_l)^T (per-set max of the layer input),
  *   actor dLambda3 = sum_sets GA3, dGamma3 = -(sum_r dlogits)^T MAX2A,
  *   critic dLambda3 = (dmean / R)^T CS2, dGamma3 = -dmean^T MAX2C.
- * The pooled gradient goes to the first row attaining the set-wise max (torch.max). */
+ * The pooled gradient goes to the first row attaining the set-wise max (torch.max).  Layer
+ * 1's pooled term is left to the caller: dz1 at row ID1[o] of feature o also carries
+ * -V[o] act'(MAX1[o]) (V = Gamma2^T sum_r dz2, per set), so GS1 -= V act'(MAX1) and
+ * dLambda1 -= sum_sets (V act'(MAX1))^T obs[ID1] (act' = ReLU' actor, ELU' critic). */
 #define LB_DS_BWD_FLOATS 24704
-#define LB_DS_SETVEC_FLOATS 648
+#define LB_DS_SETVEC_FLOATS 840
 #define LB_DS_WGRAD_FLOATS 4608  /* per head: dLambda2 [64][64] then dLambda1 [64][8] */
 #define LB_DS_WORKSPACE_FLOATS (1024 * 2 * LB_DS_WGRAD_FLOATS)
 /* per-set vector offsets (floats) inside a LB_DS_SETVEC_FLOATS row */
@@ -268,13 +272,21 @@ int lb_replay_add(int64_t num_envs, int32_t obs_floats, int64_t slots, const int
 #define LB_DSV_GS2C 456
 #define LB_DSV_MAX1C 520
 #define LB_DSV_GS1C 584
+#define LB_DSV_ID1A 648  /* [64] u8 first argmax rows (16 floats of bytes) */
+#define LB_DSV_ID2A 664
+#define LB_DSV_ID1C 680
+#define LB_DSV_ID2C 696
+#define LB_DSV_VA 712    /* [64] Gamma2^T sum_r dz2 (actor) */
+#define LB_DSV_VC 776    /* [64] (critic) */
 
 /* obs [B,R,8] -> logits_out [B,R] (actor; NULL = skip), psi_mean_out [B,64] (critic psi
  * averaged over the set; NULL = skip), save_actor [2,B,R,64] (h1 after ReLU, h2 after ELU),
- * save_critic [2,B,R,64] (c1, c2 after ELU).  frag: lb_ds_pack's image. */
+ * save_critic [2,B,R,64] (c1, c2 after ELU), setvec_out [B, LB_DS_SETVEC_FLOATS] (MAX0 and
+ * each head's MAX1, MAX2, ID1, ID2; the backward fills in the rest).  frag: lb_ds_pack's
+ * image. */
 int lb_ds_train_forward(const float* frag, const float* obs, int64_t num_envs, int32_t num_elements,
                         float* logits_out, float* psi_mean_out, float* save_actor, float* save_critic,
-                        void* stream);
+                        float* setvec_out, void* stream);
 
 /* PPO loss head (envs/ppo_deepset.py:227-263) for M sets of R <= 128 elements: per-set
  * terms [M,6] (policy term max(pg1, pg2), value term, entropy, approx-kl term, clipped
@@ -292,7 +304,8 @@ int lb_ds_pack_backward(const lb_ds_weights* w, float* bwd_frag_out, void* strea
 
 /* dlogits [B,R] (NULL = no actor), dmean [B,64] (NULL = no critic) -> wgrad_out
  * [2, LB_DS_WGRAD_FLOATS] (actor, critic: dLambda2, dLambda1; a head not asked for gets
- * zeros) and setvec [B, LB_DS_SETVEC_FLOATS]; workspace [LB_DS_WORKSPACE_FLOATS] is
+ * zeros) and setvec [B, LB_DS_SETVEC_FLOATS] (in: lb_ds_train_forward's fields; out: GA3 /
+ * CS2, GS2, GS1, V); workspace [LB_DS_WORKSPACE_FLOATS] is
  * scratch (per-wave partial sums, reduced in a fixed order: results do not depend on B's
  * split over waves beyond float summation order). */
 int lb_ds_train_backward(const float* bwd_frag, const float* obs, int64_t num_envs, int32_t num_elements,

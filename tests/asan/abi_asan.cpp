@@ -87,7 +87,7 @@ int main() {
     CHECK(lb_ds_pack(nullptr, nullptr, nullptr) != 0);
     CHECK(lb_ds_forward(nullptr, nullptr, 1, 9, nullptr, nullptr, nullptr) != 0);
     CHECK(lb_ds_q_argmax(nullptr, nullptr, 1, 9, nullptr, nullptr, nullptr, nullptr) != 0);
-    CHECK(lb_ds_train_forward(nullptr, nullptr, 1, 9, nullptr, nullptr, nullptr, nullptr, nullptr) != 0);
+    CHECK(lb_ds_train_forward(nullptr, nullptr, 1, 9, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr) != 0);
     CHECK(lb_ds_pack_backward(nullptr, nullptr, nullptr) != 0);
     CHECK(lb_ds_train_backward(nullptr, nullptr, 1, 9, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                                nullptr) != 0);
@@ -104,7 +104,7 @@ int main() {
     CHECK(lb_ds_forward((const float*)fake, (const float*)fake, 1, LB_DS_MAX_ELEMENTS_FWD + 1, (float*)fake, nullptr,
                         nullptr) != 0);
     CHECK(lb_ds_train_forward((const float*)fake, (const float*)fake, 1, LB_DS_MAX_ELEMENTS + 1, (float*)fake,
-                              nullptr, (float*)fake, nullptr, nullptr) != 0);
+                              nullptr, (float*)fake, nullptr, (float*)fake, nullptr) != 0);
     {
         lb_config t = base_cfg();
         t.rng_mode = LB_RNG_TRACE;

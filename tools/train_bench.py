@@ -68,7 +68,7 @@ def main():
 
         def f():
             _native.check(L.lb_ds_train_forward(frag.data_ptr(), x.data_ptr(), B, R, logits.data_ptr(),
-                                                mean.data_ptr(), sa.data_ptr(), sc.data_ptr(), st))
+                                                mean.data_ptr(), sa.data_ptr(), sc.data_ptr(), sv.data_ptr(), st))
 
         def b():
             _native.check(L.lb_ds_train_backward(bfrag.data_ptr(), x.data_ptr(), B, R, sa.data_ptr(), sc.data_ptr(),
