@@ -763,20 +763,9 @@ int lb_ds_train_backward(const float* bwd_frag, const float* obs, int64_t num_en
                   num_envs, num_elements, actor, critic};
     // fixed grid: one workspace slot per block, so the reduction order never depends on B
     hipStream_t s = (hipStream_t)stream;
-    const int nct = ((num_elements - 1) % 16) / 4 + 1;  // 4-row groups in the last 16-row tile
-    if (actor) {
-        if (nct == 1) hipLaunchKernelGGL((k_ds_train_bwd<0, 1>), dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);
-        else if (nct == 2) hipLaunchKernelGGL((k_ds_train_bwd<0, 2>), dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);
-        else if (nct == 3) hipLaunchKernelGGL((k_ds_train_bwd<0, 3>), dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);
-        else hipLaunchKernelGGL((k_ds_train_bwd<0, 4>), dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);
-    }
+    if (actor) hipLaunchKernelGGL(k_ds_train_bwd<0>, dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);
     if (int r = check_launch()) return r;
-    if (critic) {
-        if (nct == 1) hipLaunchKernelGGL((k_ds_train_bwd<1, 1>), dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);
-        else if (nct == 2) hipLaunchKernelGGL((k_ds_train_bwd<1, 2>), dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);
-        else if (nct == 3) hipLaunchKernelGGL((k_ds_train_bwd<1, 3>), dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);
-        else hipLaunchKernelGGL((k_ds_train_bwd<1, 4>), dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);
-    }
+    if (critic) hipLaunchKernelGGL(k_ds_train_bwd<1>, dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);
     if (int r = check_launch()) return r;
     static_assert(DSW_SLOTS % (2 * DSR_GROUPS) == 0, "reduction stride");
     hipLaunchKernelGGL(k_ds_wgrad_reduce, dim3((2 * DSW_FLOATS + DSR_COLS - 1) / DSR_COLS), dim3(DSR_COLS * DSR_GROUPS),

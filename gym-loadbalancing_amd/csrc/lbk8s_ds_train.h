@@ -27,8 +27,6 @@
 // holds features 16(k >> 2) + 4(l >> 4) + (k & 3)).
 #pragma once
 
-#include <type_traits>
-
 #include "lbk8s_deepsets.h"
 
 namespace lbk {
@@ -66,7 +64,7 @@ static_assert(DSV_MAX1A == LB_DSV_MAX1A && DSV_MAX2A == LB_DSV_MAX2A && DSV_MAX1
                   DSV_MAX0 == LB_DSV_MAX0,
               "per-set vector layout and header disagree");
 
-constexpr int DSB_BLOCK = 256;                       // 4 waves: 1 per SIMD, one block per CU
+constexpr int DSB_BLOCK = 512;                       // 8 waves: 2 per SIMD, one block per CU
 constexpr int DSW_FLOATS = 4608;                     // per head: dLambda2 [64][64], dLambda1 [64][8]
 constexpr int DSW_GRID = 256;                        // fixed grid (any B): one block per CU
 constexpr int DSW_SLOTS = DSW_GRID;                  // one partial-sum slot per block
@@ -94,7 +92,8 @@ __device__ __forceinline__ float dact(float y) {
 
 // ---- the backward kernel
 //
-// One wave per SIMD (4 per CU, 512 registers each).  A wave walks its sets (env0, env0 +
+// Two waves per SIMD (8 per CU, 256 registers each: one wave's vector and memory work
+// issues while the other's matrix instructions run).  A wave walks its sets (env0, env0 +
 // nwaves, ...) 16 rows at a time.  The set-wise maxima and their first argmax rows come
 // from the training forward (setvec MAX*, ID*), so each set is read once:
 //   per set, before its first tile: the set vectors c1, c2 (below), from the actor's
@@ -110,8 +109,7 @@ __device__ __forceinline__ float dact(float y) {
 //   per set, after its last tile: sum_r dz2 in closed form, V = Gamma2^T sum_r dz2, the set
 //     sums out.  Layer 1's pooled term (dz1 at row ID1[o] of feature o carries -V[o]
 //     act'(MAX1[o])) is the caller's (lbk8s.h): it touches one row per feature.
-// Every step loads the next step's tile before it computes (two buffers, used alternately),
-// and each set's small inputs (dlogits or dmean, ID2, MAX2) are loaded one set ahead.
+// Each set's small inputs (dlogits or dmean, ID2, MAX2) are loaded one set ahead.
 //
 // Per feature o, dz2[r][o] = (c1[o] - [r == ID2[o]] c2[o]) elu'(h2[r][o]) with actor
 // c1 = dl[r] Lambda3[o] (row-dependent through dl), c2 = g3 Gamma3[o];
@@ -184,10 +182,8 @@ __device__ __forceinline__ float matvec64(const float* M, const float* x, int la
     return acc;
 }
 
-// One launch per head (HEAD 0 actor, 1 critic).  NCT: 4-row groups of the last tile that
-// hold set rows (ceil(((R - 1) % 16 + 1) / 4)); the last tile's weight-gradient products
-// skip the groups past R.
-template <int HEAD, int NCT>
+// One launch per head (HEAD 0 actor, 1 critic).
+template <int HEAD>
 __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
     constexpr int ACT1 = HEAD == 0 ? 1 : 2;  // activation after layer 1: ReLU (actor) / ELU (critic)
     // natural-order weights [i][o] (W[out i][in o]): Gamma2 at 0; the critic's Lambda3,
@@ -224,6 +220,7 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
     float* la = TB[wv];
     float* cv = CV[wv];
     const int R = p.R, ntl = (R + 15) / 16;
+    const int nct = ((R - 1) % 16) / 4 + 1;  // 4-row groups of the last tile that hold set rows
     const int col = lane & 15, grp = lane >> 4;
     const int64_t plane = p.B * (int64_t)R * 64;
     const float* in1 = HEAD == 0 ? p.save_actor : p.save_critic;  // h1 / c1
@@ -305,9 +302,10 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
             for (int m = 0; m < 4; ++m) S4[m] = G4[m] = gs1[m] = 0.f;
         };
         // one 16-row tile of the current set
-        auto compute = [&](int t, Tile2& c, auto ncc) {
+        // nc: the tile's 4-row groups that hold set rows (the weight-gradient products skip
+        // the others)
+        auto compute = [&](int t, Tile2& c, int nc) {
 #pragma clang fp contract(fast)
-            constexpr int NC = decltype(ncc)::value;  // 4-row groups with set rows
             // Lambda2^T and the set vectors re-read from LDS per tile: an opaque offset keeps
             // the compiler from hoisting the loop-invariant reads into registers
             uint32_t wo = 0;
@@ -346,7 +344,8 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
             }
             // dLambda2 += dz2^T h1 straight from registers (W layout = the MFMA operands)
 #pragma unroll
-            for (int cs = 0; cs < NC; ++cs) {
+            for (int cs = 0; cs < 4; ++cs) {
+                if (cs >= nc) break;
                 const float av[4] = {dz[cs].x, dz[cs].y, dz[cs].z, dz[cs].w};
                 const float bv[4] = {c.h[cs].x, c.h[cs].y, c.h[cs].z, c.h[cs].w};
 #pragma unroll
@@ -405,7 +404,7 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
                     d1[m] = ACT1 == 1 ? (ha[m] > 0.f ? pa[m] : 0.f) : pa[m] * fminf(ha[m], 0.f) + pa[m];
                     gs1[m] += d1[m];
                 }
-                if (cc < NC) {
+                if (cc < nc) {
                     const float xv = col < 8 ? c.x[cc] : 0.f;
 #pragma unroll
                     for (int mt = 0; mt < 4; ++mt) w1[mt] = mfma4(d1[mt], xv, w1[mt]);
@@ -413,34 +412,24 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
             }
         };
 
-        // the stream of tiles g = j * ntl + t, j < n; two tile buffers used alternately
+        // the stream of tiles g = j * ntl + t, j < n
         const int64_t steps = n * ntl;
         int64_t j = 0;
         int t = 0;
-        Tile2 A, B;
-        load_tile2<HEAD>(p, in1, in2, env_of(0), 0, col, grp, A);
-        auto step = [&](Tile2& cur, Tile2& nxt, bool more) {
-            int tn = t + 1;
-            int64_t jn = j;
-            if (tn == ntl) {
-                tn = 0;
-                ++jn;
-            }
+        auto step = [&]() {
             if (t == 0) prologue(j);
-            if (more) load_tile2<HEAD>(p, in1, in2, env_of(jn), tn, col, grp, nxt);
-            if (NCT < 4 && t == ntl - 1)
-                compute(t, cur, std::integral_constant<int, NCT>{});
-            else
-                compute(t, cur, std::integral_constant<int, 4>{});
-            if (tn == 0) epilogue(j);
-            t = tn;
-            j = jn;
+            Tile2 cur;
+            load_tile2<HEAD>(p, in1, in2, env_of(j), t, col, grp, cur);
+            compute(t, cur, t == ntl - 1 ? nct : 4);
+            if (t == ntl - 1) {
+                epilogue(j);
+                t = 0;
+                ++j;
+            } else {
+                ++t;
+            }
         };
-        for (int64_t g = 0; g + 1 < steps; g += 2) {
-            step(A, B, true);
-            step(B, A, g + 2 < steps);
-        }
-        if (steps & 1) step(A, B, false);
+        for (int64_t g = 0; g < steps; ++g) step();
     }
     // the block's waves summed in LDS in a fixed order, one slot per block
     __syncthreads();
