@@ -763,10 +763,19 @@ int lb_ds_train_backward(const float* bwd_frag, const float* obs, int64_t num_en
                   num_envs, num_elements, actor, critic};
     // fixed grid: one workspace slot per block, so the reduction order never depends on B
     hipStream_t s = (hipStream_t)stream;
-    if (actor) hipLaunchKernelGGL(k_ds_train_bwd<0>, dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);
-    if (int r = check_launch()) return r;
-    if (critic) hipLaunchKernelGGL(k_ds_train_bwd<1>, dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);
-    if (int r = check_launch()) return r;
+    // each head: the backward, then layer 1's pooled term added to its slots
+    if (actor) {
+        hipLaunchKernelGGL(k_ds_train_bwd<0>, dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);
+        if (int r = check_launch()) return r;
+        hipLaunchKernelGGL(k_ds_l1_pool<0>, dim3(DSW_GRID), dim3(64 * DSL_SUB), 0, s, p);
+        if (int r = check_launch()) return r;
+    }
+    if (critic) {
+        hipLaunchKernelGGL(k_ds_train_bwd<1>, dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);
+        if (int r = check_launch()) return r;
+        hipLaunchKernelGGL(k_ds_l1_pool<1>, dim3(DSW_GRID), dim3(64 * DSL_SUB), 0, s, p);
+        if (int r = check_launch()) return r;
+    }
     static_assert(DSW_SLOTS % (2 * DSR_GROUPS) == 0, "reduction stride");
     hipLaunchKernelGGL(k_ds_wgrad_reduce, dim3((2 * DSW_FLOATS + DSR_COLS - 1) / DSR_COLS), dim3(DSR_COLS * DSR_GROUPS),
                        0, s, workspace, wgrad_out, (int)actor, (int)critic);

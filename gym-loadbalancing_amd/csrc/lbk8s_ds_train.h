@@ -54,13 +54,13 @@ enum : int {
     DSV_ID2A = 664,
     DSV_ID1C = 680,
     DSV_ID2C = 696,
-    DSV_VA = 712,     // actor: Gamma2^T sum_r dz2 (layer 1's pooled term, applied by the caller)
-    DSV_VC = 776,     // critic
+    DSV_P1A = 712,    // actor: layer 1's pooled term per feature, V act'(MAX1) (k_ds_l1_pool)
+    DSV_P1C = 776,    // critic
     DSV_FLOATS = 840,
 };
 static_assert(DSV_MAX1A == LB_DSV_MAX1A && DSV_MAX2A == LB_DSV_MAX2A && DSV_MAX1C == LB_DSV_MAX1C &&
                   DSV_MAX2C == LB_DSV_MAX2C && DSV_ID1A == LB_DSV_ID1A && DSV_ID2A == LB_DSV_ID2A &&
-                  DSV_ID1C == LB_DSV_ID1C && DSV_ID2C == LB_DSV_ID2C && DSV_VA == LB_DSV_VA && DSV_VC == LB_DSV_VC &&
+                  DSV_ID1C == LB_DSV_ID1C && DSV_ID2C == LB_DSV_ID2C && DSV_P1A == LB_DSV_P1A && DSV_P1C == LB_DSV_P1C &&
                   DSV_MAX0 == LB_DSV_MAX0,
               "per-set vector layout and header disagree");
 
@@ -106,9 +106,10 @@ __device__ __forceinline__ float dact(float y) {
 //     features: dz2 goes through a per-wave LDS transpose into the MFMA's other operand
 //     layout and the result back, Lambda2^T from LDS); dLambda1; the set sums S, G of h2
 //     terms and of dz1;
-//   per set, after its last tile: sum_r dz2 in closed form, V = Gamma2^T sum_r dz2, the set
-//     sums out.  Layer 1's pooled term (dz1 at row ID1[o] of feature o carries -V[o]
-//     act'(MAX1[o])) is the caller's (lbk8s.h): it touches one row per feature.
+//   per set, after its last tile: sum_r dz2 in closed form, V = Gamma2^T sum_r dz2, layer
+//     1's pooled term (dz1 at row ID1[o] of feature o carries -V[o] act'(MAX1[o]): one row
+//     per feature, folded into sum_r dz1 here and into dLambda1 by k_ds_l1_pool), the set
+//     sums out.
 // Each set's small inputs (dlogits or dmean, ID2, MAX2) are loaded one set ahead.
 //
 // Per feature o, dz2[r][o] = (c1[o] - [r == ID2[o]] c2[o]) elu'(h2[r][o]) with actor
@@ -136,6 +137,7 @@ struct SetIn {
     float dm;        // critic: dmean[lane]
     int id2;         // ID2 bytes of features 4col .. 4col + 3
     float4 mx2;      // MAX2 of features 4col .. 4col + 3
+    float mx1;       // MAX1 of feature lane
 };
 
 template <int HEAD>
@@ -165,6 +167,7 @@ __device__ __forceinline__ void load_setin(const DSBwdParams& p, int64_t env, in
     }
     s.id2 = *reinterpret_cast<const int*>(reinterpret_cast<const uint8_t*>(sv + (HEAD == 0 ? DSV_ID2A : DSV_ID2C)) + 4 * col);
     s.mx2 = *reinterpret_cast<const float4*>(sv + (HEAD == 0 ? DSV_MAX2A : DSV_MAX2C) + 4 * col);
+    s.mx1 = sv[(HEAD == 0 ? DSV_MAX1A : DSV_MAX1C) + lane];
 }
 
 // lane-per-feature matrix-vector product out[lane] = sum_i M[i][lane] x[i], M natural
@@ -240,6 +243,7 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
         float S4[4], G4[4], gs1[4], g3 = 0.f;
         int id2w = 0;
         float4 mx2v;
+        float mx1l = 0.f;
 #pragma unroll
         for (int m = 0; m < 4; ++m) S4[m] = G4[m] = gs1[m] = 0.f;
         SetIn pre;
@@ -251,6 +255,7 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
             if (j + 1 < n) load_setin<HEAD>(p, env_of(j + 1), lane, col, pre);
             id2w = cur.id2;
             mx2v = cur.mx2;
+            mx1l = cur.mx1;
             float c1, c2;
             if (HEAD == 0) {
                 float s = cur.dl0 + cur.dl1;
@@ -293,11 +298,23 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
                     make_float4(gs[0], gs[1], gs[2], gs[3]);
                 *reinterpret_cast<float4*>(sv + (HEAD == 0 ? DSV_GA3 : DSV_CS2) + 4 * col) =
                     make_float4(G4[0], G4[1], G4[2], G4[3]);
-                *reinterpret_cast<float4*>(sv + (HEAD == 0 ? DSV_GS1A : DSV_GS1C) + 4 * col) =
-                    make_float4(gs1[0], gs1[1], gs1[2], gs1[3]);
                 *reinterpret_cast<float4*>(cv + 4 * col) = make_float4(gs[0], gs[1], gs[2], gs[3]);
             }
-            sv[(HEAD == 0 ? DSV_VA : DSV_VC) + lane] = matvec64(NAT, cv, lane);
+            // layer 1's pooled term: dz1 at row ID1[o] of feature o also carries -v[o]
+            // act'(MAX1[o]) with v = Gamma2^T sum_r dz2 (h1 at that row is the max); it
+            // changes that row's share of sum_r dz1 and of dLambda1 (its obs row)
+            const float v = matvec64(NAT, cv, lane);
+            const float corr = v * dact<ACT1>(mx1l);
+            cv[lane] = corr;
+            const float4 cw = *reinterpret_cast<const float4*>(cv + 4 * col);
+            gs1[0] -= cw.x;
+            gs1[1] -= cw.y;
+            gs1[2] -= cw.z;
+            gs1[3] -= cw.w;
+            if (grp == 0)
+                *reinterpret_cast<float4*>(sv + (HEAD == 0 ? DSV_GS1A : DSV_GS1C) + 4 * col) =
+                    make_float4(gs1[0], gs1[1], gs1[2], gs1[3]);
+            sv[(HEAD == 0 ? DSV_P1A : DSV_P1C) + lane] = corr;  // -> k_ds_l1_pool (dLambda1)
 #pragma unroll
             for (int m = 0; m < 4; ++m) S4[m] = G4[m] = gs1[m] = 0.f;
         };
@@ -390,7 +407,7 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt)
                 T4[col * 16 + ((4 * nt + grp) ^ col)] = make_float4(eacc[nt][0], eacc[nt][1], eacc[nt][2], eacc[nt][3]);
-            // dz1 = pre act'(h1) (W layout; the pooled term is the caller's), its set sum,
+            // dz1 = pre act'(h1) (W layout; the pooled term is added per set), its set sum,
             // dLambda1 += dz1^T obs (B columns 8..15 zero)
 #pragma unroll
             for (int cc = 0; cc < 4; ++cc) {
@@ -459,6 +476,52 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
     }
     float* slot = p.wpart + (int64_t)blockIdx.x * (2 * DSW_FLOATS) + HEAD * DSW_FLOATS;
     for (int i = threadIdx.x; i < DSW_FLOATS; i += DSB_BLOCK) slot[i] = red[i];
+}
+
+// Layer 1's pooled term in dLambda1: dz1 at row ID1[o] of feature o carries -P1[o] (the
+// backward's per-set P1 = V act'(MAX1)), so dLambda1[o][c] -= sum_sets P1[o] obs[ID1[o]][c].
+// Block b adds its share to workspace slot b of the head (after k_ds_train_bwd wrote it):
+// thread (o, sub) walks sets sub, sub + DSL_SUB, ... of the block's, two sets per iteration
+// (independent gathers in flight), 8 accumulators; the subgroups are summed in LDS in a
+// fixed order.
+constexpr int DSL_SUB = 16;  // set subgroups per block (1,024 threads)
+template <int HEAD>
+__global__ __launch_bounds__(64 * DSL_SUB) void k_ds_l1_pool(DSBwdParams p) {
+    __shared__ float part[DSL_SUB][512];
+    const int o = threadIdx.x & 63, sub = threadIdx.x >> 6;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int64_t stride = (int64_t)gridDim.x * DSL_SUB;
+    auto term = [&](int64_t s) {
+        const float* sv = p.setvec + s * (int64_t)DSV_FLOATS;
+        const float c = sv[(HEAD == 0 ? DSV_P1A : DSV_P1C) + o];
+        const int r = reinterpret_cast<const uint8_t*>(sv + (HEAD == 0 ? DSV_ID1A : DSV_ID1C))[o];
+        const float4* x = reinterpret_cast<const float4*>(p.obs + (s * (int64_t)p.R + r) * 8);
+        const float4 x0 = x[0], x1 = x[1];
+        acc[0] += c * x0.x;
+        acc[1] += c * x0.y;
+        acc[2] += c * x0.z;
+        acc[3] += c * x0.w;
+        acc[4] += c * x1.x;
+        acc[5] += c * x1.y;
+        acc[6] += c * x1.z;
+        acc[7] += c * x1.w;
+    };
+    int64_t s = (int64_t)blockIdx.x * DSL_SUB + sub;
+    for (; s + stride < p.B; s += 2 * stride) {
+        term(s);
+        term(s + stride);
+    }
+    if (s < p.B) term(s);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) part[sub][o * 8 + k] = acc[k];
+    __syncthreads();
+    float* slot = p.wpart + (int64_t)blockIdx.x * (2 * DSW_FLOATS) + HEAD * DSW_FLOATS + 4096;
+    if (threadIdx.x < 512) {
+        float t = 0.f;
+#pragma unroll
+        for (int g = 0; g < DSL_SUB; ++g) t += part[g][threadIdx.x];
+        slot[threadIdx.x] -= t;
+    }
 }
 
 // sum of the per-wave partials: out[j] = sum_s wpart[s][j], j < 2 * DSW_FLOATS; zeros for

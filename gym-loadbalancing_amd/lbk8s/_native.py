@@ -61,7 +61,7 @@ LB_DS_WGRAD_FLOATS = 4608
 LB_DS_WORKSPACE_FLOATS = 1024 * 2 * LB_DS_WGRAD_FLOATS
 LB_DSV = {"MAX0": 0, "GA3": 8, "MAX2A": 72, "GS2A": 136, "MAX1A": 200, "GS1A": 264, "CS2": 328,
           "MAX2C": 392, "GS2C": 456, "MAX1C": 520, "GS1C": 584, "ID1A": 648, "ID2A": 664, "ID1C": 680,
-          "ID2C": 696, "VA": 712, "VC": 776}
+          "ID2C": 696, "P1A": 712, "P1C": 776}
 
 _lib = None
 

@@ -17,11 +17,8 @@ sets — runs in torch:
     critic dLambda3 = (dmean / R)^T sum_r c2[r]          dGamma3 = -dmean^T max_set(c2)
 
 The pooled gradient goes to the first row attaining the max, like torch.max in the
-reference's autograd.  The forward kernel records each layer input's set-wise max and that
-row (ID1, ID2); layer 1's pooled term touches one row per feature (dz1[ID1[o]][o] carries
--V[o] act'(MAX1[o]), V = Gamma2^T sum_r dz2 from the backward) and is added here:
-
-    GS1 -= V act'(MAX1)        dLambda1 -= sum_sets (V act'(MAX1))^T obs[ID1]  Covered geometry: 8 input features, 64 hidden, 1 <= R <= 80, on a
+reference's autograd; the forward kernel records each layer input's set-wise max and that
+row for the backward.  Covered geometry: 8 input features, 64 hidden, 1 <= R <= 80, on a
 HIP device; `supported()` says whether an input qualifies.
 """
 import ctypes as C
@@ -87,22 +84,6 @@ def _over_sets(a, b):
     return out
 
 
-def _ids(setvec, name):
-    """The u8 argmax rows of a setvec field, as int64 (B, 64)."""
-    o = 4 * DSV[name]
-    return setvec.view(torch.uint8)[:, o:o + 64].long()
-
-
-def _pooled1(x, setvec, dl1, head, relu):
-    """Layer 1's pooled term for one head: (dLambda1, per-set sum of dz1) with the term of
-    the argmax row added (dz1[ID1[o]][o] -= V[o] act'(MAX1[o]))."""
-    mx1 = _vec(setvec, "MAX1" + head)
-    dact = (mx1 > 0).float() if relu else torch.where(mx1 > 0, torch.ones_like(mx1), mx1 + 1)
-    corr = _vec(setvec, "V" + head) * dact                                          # (B, 64)
-    xa = torch.gather(x, 1, _ids(setvec, "ID1" + head).unsqueeze(-1).expand(-1, -1, x.shape[2]))  # (B, 64, 8)
-    return dl1 - (corr.unsqueeze(-1) * xa).sum(0), _vec(setvec, "GS1" + head) - corr
-
-
 class _FusedDeepSetsTrain(torch.autograd.Function):
     """(x, *params) -> (logits (B, R), psi_mean (B, 64) or None).
 
@@ -150,20 +131,18 @@ class _FusedDeepSetsTrain(torch.autograd.Function):
             fused._ptr(dmean), wgrad.data_ptr(), work.data_ptr(), setvec.data_ptr(), _stream(dev)))
         max0 = _vec(setvec, "MAX0", 8)
         g3 = dlogits.sum(1)
-        dl1a, gs1a = _pooled1(x, setvec, wgrad[0, 4096:].view(64, 8), "A", relu=True)
         grads = [
-            dl1a,                                                              # actor Lambda1
-            -_over_sets(gs1a, max0),                                           # actor Gamma1
+            wgrad[0, 4096:].view(64, 8),                                       # actor Lambda1
+            -_over_sets(_vec(setvec, "GS1A"), max0),                           # actor Gamma1
             wgrad[0, :4096].view(64, 64),                                      # actor Lambda2
             -_over_sets(_vec(setvec, "GS2A"), _vec(setvec, "MAX1A")),          # actor Gamma2
             _vec(setvec, "GA3").sum(0, keepdim=True),                          # actor Lambda3
             -_over_sets(g3[:, None], _vec(setvec, "MAX2A")),                   # actor Gamma3
         ]
         if critic is not None:
-            dl1c, gs1c = _pooled1(x, setvec, wgrad[1, 4096:].view(64, 8), "C", relu=False)
             grads += [
-                dl1c,                                                          # critic Lambda1
-                -_over_sets(gs1c, max0),                                       # critic Gamma1
+                wgrad[1, 4096:].view(64, 8),                                   # critic Lambda1
+                -_over_sets(_vec(setvec, "GS1C"), max0),                       # critic Gamma1
                 wgrad[1, :4096].view(64, 64),                                  # critic Lambda2
                 -_over_sets(_vec(setvec, "GS2C"), _vec(setvec, "MAX1C")),      # critic Gamma2
                 _over_sets(dmean / R, _vec(setvec, "CS2")),                    # critic Lambda3

@@ -252,10 +252,7 @@ int lb_replay_add(int64_t num_envs, int32_t obs_floats, int64_t slots, const int
  *   dGamma_l = -(per-set sum of dz_l)^T (per-set max of the layer input),
  *   actor dLambda3 = sum_sets GA3, dGamma3 = -(sum_r dlogits)^T MAX2A,
  *   critic dLambda3 = (dmean / R)^T CS2, dGamma3 = -dmean^T MAX2C.
- * The pooled gradient goes to the first row attaining the set-wise max (torch.max).  Layer
- * 1's pooled term is left to the caller: dz1 at row ID1[o] of feature o also carries
- * -V[o] act'(MAX1[o]) (V = Gamma2^T sum_r dz2, per set), so GS1 -= V act'(MAX1) and
- * dLambda1 -= sum_sets (V act'(MAX1))^T obs[ID1] (act' = ReLU' actor, ELU' critic). */
+ * The pooled gradient goes to the first row attaining the set-wise max (torch.max). */
 #define LB_DS_BWD_FLOATS 24704
 #define LB_DS_SETVEC_FLOATS 840
 #define LB_DS_WGRAD_FLOATS 4608  /* per head: dLambda2 [64][64] then dLambda1 [64][8] */
@@ -276,14 +273,14 @@ int lb_replay_add(int64_t num_envs, int32_t obs_floats, int64_t slots, const int
 #define LB_DSV_ID2A 664
 #define LB_DSV_ID1C 680
 #define LB_DSV_ID2C 696
-#define LB_DSV_VA 712    /* [64] Gamma2^T sum_r dz2 (actor) */
-#define LB_DSV_VC 776    /* [64] (critic) */
+#define LB_DSV_P1A 712   /* [64] layer 1's pooled term per feature (actor) */
+#define LB_DSV_P1C 776   /* [64] (critic) */
 
 /* obs [B,R,8] -> logits_out [B,R] (actor; NULL = skip), psi_mean_out [B,64] (critic psi
  * averaged over the set; NULL = skip), save_actor [2,B,R,64] (h1 after ReLU, h2 after ELU),
  * save_critic [2,B,R,64] (c1, c2 after ELU), setvec_out [B, LB_DS_SETVEC_FLOATS] (MAX0 and
- * each head's MAX1, MAX2, ID1, ID2; the backward fills in the rest).  frag: lb_ds_pack's
- * image. */
+ * each head's MAX1, MAX2, ID1, ID2; the backward reads them and fills in the rest).
+ * frag: lb_ds_pack's image. */
 int lb_ds_train_forward(const float* frag, const float* obs, int64_t num_envs, int32_t num_elements,
                         float* logits_out, float* psi_mean_out, float* save_actor, float* save_critic,
                         float* setvec_out, void* stream);
@@ -305,7 +302,7 @@ int lb_ds_pack_backward(const lb_ds_weights* w, float* bwd_frag_out, void* strea
 /* dlogits [B,R] (NULL = no actor), dmean [B,64] (NULL = no critic) -> wgrad_out
  * [2, LB_DS_WGRAD_FLOATS] (actor, critic: dLambda2, dLambda1; a head not asked for gets
  * zeros) and setvec [B, LB_DS_SETVEC_FLOATS] (in: lb_ds_train_forward's fields; out: GA3 /
- * CS2, GS2, GS1, V); workspace [LB_DS_WORKSPACE_FLOATS] is
+ * CS2, GS2, GS1, P1); workspace [LB_DS_WORKSPACE_FLOATS] is
  * scratch (per-wave partial sums, reduced in a fixed order: results do not depend on B's
  * split over waves beyond float summation order). */
 int lb_ds_train_backward(const float* bwd_frag, const float* obs, int64_t num_envs, int32_t num_elements,
