@@ -155,50 +155,71 @@ __device__ __forceinline__ void set_max_batched(const float (&h)[P * TS][KS], fl
     }
 }
 
-// training forward: each env's set-wise max of a layer input per feature (mb from
-// set_max_batched) and, with IDS, its FIRST argmax row (torch.max's index: the smallest
-// row holding the max) into setvec; lane col == s stores env s.  KS = 16: feature
-// 16(k >> 2) + 4grp + (k & 3); KS = 2 (the observation): feature 4k + grp.
-template <int TS, int P, int KS, bool IDS>
-__device__ __forceinline__ void store_set_max(const float (&h)[P * TS][KS], const float (&mb)[KS], int col, int grp,
-                                              int R, int64_t env0, int64_t B, float* setvec, int off_max,
-                                              int off_id) {
-    constexpr int KW = KS < 4 ? KS : 4;
+// training forward: each env's set-wise max of the observation per feature (mb from
+// set_max_batched, feature 4k + grp) into setvec; lane col == s stores env s
+template <int TS, int P>
+__device__ __forceinline__ void store_obs_max(const float (&mb)[2], int col, int grp, int64_t env0, int64_t B,
+                                              float* setvec) {
 #pragma unroll
-    for (int q = 0; q < KS / KW; ++q) {
-        float M[KW * P], c[KW * P];
+    for (int s = 0; s < P; ++s) {
+        const float m0 = from_col_dyn<P>(mb[0], s), m1 = from_col_dyn<P>(mb[1], s);
+        if (col != s || env0 + s >= B) continue;
+        float* sv = setvec + (env0 + s) * (int64_t)LB_DS_SETVEC_FLOATS + LB_DSV_MAX0;
+        sv[grp] = m0;
+        sv[4 + grp] = m1;
+    }
+}
+
+// training forward: set_max_batched and the first argmax rows in one pass.  Each lane keeps
+// its max over its rows and the first row attaining it (strict > over ascending tiles);
+// the set's max is the 16 columns' max, its first row the smallest row among the lanes
+// holding it.  Both go to setvec (lane col == s stores env s), the batched max to mb.
+template <int TS, int P, int KS>
+__device__ __forceinline__ void set_max_store(const float (&h)[P * TS][KS], float (&mb)[KS], int col, int grp, int R,
+                                              int64_t env0, int64_t B, float* setvec, int off_max, int off_id) {
+    static_assert(KS == 16, "hidden layers");
+    float m[KS * P], rr[KS * P];
 #pragma unroll
-        for (int kk = 0; kk < KW; ++kk)
-#pragma unroll
-            for (int s = 0; s < P; ++s) {
-                const int k = q * KW + kk;
-                M[kk * P + s] = from_col_dyn<P>(mb[k], s);
-                if (IDS) {
-                    // descending tiles: the last hit is the first row; only the last tile can
-                    // hold rows past R
-                    float r = (16 * (TS - 1) + col < R && h[s * TS + TS - 1][k] == M[kk * P + s])
-                                  ? (float)(16 * (TS - 1) + col) : 1e9f;
-#pragma unroll
-                    for (int t = TS - 2; t >= 0; --t) r = h[s * TS + t][k] == M[kk * P + s] ? (float)(16 * t + col) : r;
-                    c[kk * P + s] = -r;
-                }
-            }
-        if (IDS) row_reduce<true>(c);
+    for (int k = 0; k < KS; ++k)
 #pragma unroll
         for (int s = 0; s < P; ++s) {
-            if (col != s || env0 + s >= B) continue;
-            float* sv = setvec + (env0 + s) * (int64_t)LB_DS_SETVEC_FLOATS;
-            if (KS == 16) {
-                const int f0 = 16 * q + 4 * grp;
-                *reinterpret_cast<float4*>(sv + off_max + f0) = make_float4(M[s], M[P + s], M[2 * P + s], M[3 * P + s]);
-                if (IDS)
-                    *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(sv + off_id) + f0) =
-                        (uint32_t)(-c[s]) | ((uint32_t)(-c[P + s]) << 8) | ((uint32_t)(-c[2 * P + s]) << 16) |
-                        ((uint32_t)(-c[3 * P + s]) << 24);
-            } else {
+            float v = -INFINITY, r = 1e9f;
 #pragma unroll
-                for (int kk = 0; kk < KW; ++kk) sv[off_max + 4 * kk + grp] = M[kk * P + s];
+            for (int t = 0; t < TS; ++t) {
+                const float x = h[s * TS + t][k];
+                const bool u = (t < TS - 1 || 16 * t + col < R) && x > v;  // only the last tile has rows past R
+                v = u ? x : v;
+                r = u ? (float)(16 * t + col) : r;
             }
+            m[k * P + s] = v;
+            rr[k * P + s] = r;
+        }
+    float M[KS * P];
+#pragma unroll
+    for (int i = 0; i < KS * P; ++i) M[i] = m[i];
+    row_reduce<true>(M);  // every lane of a row group: the max of each (feature, env)
+#pragma unroll
+    for (int i = 0; i < KS * P; ++i) m[i] = m[i] == M[i] ? -rr[i] : -1e9f;
+    row_reduce<true>(m);  // -(first row)
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+        float r = M[k * P];
+#pragma unroll
+        for (int s = 1; s < P; ++s) r = (col % P == s) ? M[k * P + s] : r;
+        mb[k] = r;
+    }
+#pragma unroll
+    for (int s = 0; s < P; ++s) {
+        if (col != s || env0 + s >= B) continue;
+        float* sv = setvec + (env0 + s) * (int64_t)LB_DS_SETVEC_FLOATS;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int f0 = 16 * q + 4 * grp;
+            *reinterpret_cast<float4*>(sv + off_max + f0) =
+                make_float4(M[(4 * q) * P + s], M[(4 * q + 1) * P + s], M[(4 * q + 2) * P + s], M[(4 * q + 3) * P + s]);
+            *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(sv + off_id) + f0) =
+                (uint32_t)(-m[(4 * q) * P + s]) | ((uint32_t)(-m[(4 * q + 1) * P + s]) << 8) |
+                ((uint32_t)(-m[(4 * q + 2) * P + s]) << 16) | ((uint32_t)(-m[(4 * q + 3) * P + s]) << 24);
         }
     }
 }
@@ -286,19 +307,19 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
         }
         float m0[2];
         set_max_batched<TS, P, 2>(h0, m0, col, R);
-        if (TRAIN) store_set_max<TS, P, 2, false>(h0, m0, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX0, 0);
+        if (TRAIN) store_obs_max<TS, P>(m0, col, grp, env0, p.B, p.setvec);
 
         float h1[P * TS][16], m1[16], h2[P * TS][16], m2[16];
         // ---- actor: Eq(8->64) ReLU Eq(64->64) ELU Eq(64->1)
         if (p.actor) {
             eq_layer<TS, P, 2, 1>(W + DS_A1L, W + DS_A1G, h0, m0, h1, lane);
             if (TRAIN) store_rows<TS, P>(p.save_actor, h1, env0, p.B, R, col, grp);
-            set_max_batched<TS, P, 16>(h1, m1, col, R);
-            if (TRAIN) store_set_max<TS, P, 16, true>(h1, m1, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX1A, LB_DSV_ID1A);
+            if (TRAIN) set_max_store<TS, P, 16>(h1, m1, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX1A, LB_DSV_ID1A);
+            else set_max_batched<TS, P, 16>(h1, m1, col, R);
             eq_layer<TS, P, 16, 2>(W + DS_A2L, W + DS_A2G, h1, m1, h2, lane);
             if (TRAIN) store_rows<TS, P>(p.save_actor + p.B * (int64_t)R * 64, h2, env0, p.B, R, col, grp);
-            set_max_batched<TS, P, 16>(h2, m2, col, R);
-            if (TRAIN) store_set_max<TS, P, 16, true>(h2, m2, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX2A, LB_DSV_ID2A);
+            if (TRAIN) set_max_store<TS, P, 16>(h2, m2, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX2A, LB_DSV_ID2A);
+            else set_max_batched<TS, P, 16>(h2, m2, col, R);
             // layer 3 (64 -> 1) on the VALU: a 16-row output tile would use 1/16 of an MFMA.
             // Lane (col, grp) dots its 16 features with Lambda3 / -Gamma3 (row 0 of the
             // fragments: column 0 of its row group), then the 4 row groups are summed.
@@ -356,12 +377,12 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
         // ---- critic: psi = Eq ELU Eq ELU Eq, mean over the set, rho = Linear ELU Linear
         eq_layer<TS, P, 2, 2>(W + DS_C1L, W + DS_C1G, h0, m0, h1, lane);
         if (TRAIN) store_rows<TS, P>(p.save_critic, h1, env0, p.B, R, col, grp);
-        set_max_batched<TS, P, 16>(h1, m1, col, R);
-        if (TRAIN) store_set_max<TS, P, 16, true>(h1, m1, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX1C, LB_DSV_ID1C);
+        if (TRAIN) set_max_store<TS, P, 16>(h1, m1, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX1C, LB_DSV_ID1C);
+        else set_max_batched<TS, P, 16>(h1, m1, col, R);
         eq_layer<TS, P, 16, 2>(W + DS_C2L, W + DS_C2G, h1, m1, h2, lane);
         if (TRAIN) store_rows<TS, P>(p.save_critic + p.B * (int64_t)R * 64, h2, env0, p.B, R, col, grp);
-        set_max_batched<TS, P, 16>(h2, m2, col, R);
-        if (TRAIN) store_set_max<TS, P, 16, true>(h2, m2, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX2C, LB_DSV_ID2C);
+        if (TRAIN) set_max_store<TS, P, 16>(h2, m2, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX2C, LB_DSV_ID2C);
+        else set_max_batched<TS, P, 16>(h2, m2, col, R);
         // layer 3 has no activation and only its mean over the set is used, so
         // mean_r(Lambda3 c2[r] - Gamma3 max(c2)) = Lambda3 mean_r(c2) - Gamma3 max(c2): one
         // matrix-vector pair on the batched (column c = env c mod P) operands instead of a
