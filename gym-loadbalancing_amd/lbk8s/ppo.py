@@ -21,6 +21,7 @@ same stream (the collective stays outside the captures, so any backend works).  
 capture's warm-up steps are undone (parameters restored, Adam state zeroed), so the graph
 path computes the same update as the eager one.
 """
+import os
 import time
 from typing import Optional
 
@@ -128,7 +129,9 @@ class PPO_DeepSets:
         self.use_graphs = bool(use_graphs) and self.batch_size % self.minibatch_size == 0
         if self.use_graphs:
             self._lr = torch.tensor(float(learning_rate), device=self.device)
-            self.optimizer = optim.Adam(self.agent.parameters(), lr=self._lr, eps=1e-5, capturable=True)
+            # torch's fused (single multi-tensor kernel) Adam: fewer launches per captured step
+            self.optimizer = optim.Adam(self.agent.parameters(), lr=self._lr, eps=1e-5, capturable=True,
+                                        fused=os.environ.get("LBK8S_FUSED_ADAM", "1") == "1")
         else:
             self.optimizer = optim.Adam(self.agent.parameters(), lr=learning_rate, eps=1e-5)
         self._mb_graphs = None
