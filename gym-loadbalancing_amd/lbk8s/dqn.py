@@ -13,6 +13,7 @@ Multi-GPU: gradients averaged with one all_reduce per train step (RCCL); every r
 its own envs and replay; the logged episode return is the mean over every rank's finished
 episodes (one 2-double all_reduce per log line).
 """
+import os
 import random
 import time
 from copy import deepcopy
@@ -134,7 +135,10 @@ class DQN_DeepSets:
         if lbdist.is_multi():
             lbdist.broadcast_parameters(self.q_network)  # replicas start from rank 0's weights
         self.target_network = deepcopy(self.q_network)
-        self.optimizer = optim.Adam(self.q_network.parameters(), lr=learning_rate)
+        # on a HIP device, torch's fused Adam: one multi-tensor kernel per train step
+        self.optimizer = optim.Adam(self.q_network.parameters(), lr=learning_rate,
+                                    fused=(self.device.type == "cuda" and os.environ.get("LBK8S_FUSED_ADAM", "1") == "1")
+                                    or None)
         self.rb = DeviceReplayBuffer(buffer_size, self.num_envs, env.observation_space.shape, self.device, self.gen)
         self._act = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
         self._done_u8 = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
