@@ -170,3 +170,33 @@ def test_philox_many_envs_matches_oracle(oracle_mod, name):
             np.testing.assert_array_equal(env.terminal_obs.cpu().numpy()[d1], t2[d1])
     np.testing.assert_array_equal(env.field("avg_load_served").cpu().numpy(), orc.field("loads"))
     assert env.status() == 0
+
+
+@pytest.mark.gpu
+def test_config2_rollout_matches_oracle(oracle_mod):
+    """BASELINE config 2 at its size: 4096 default envs under the env's own random policy,
+    run as lb_rollout launches of 50 vector steps (the config-2 fast path), == the C oracle
+    stepping one vector step at a time with its random policy, bit for bit, across the
+    auto-resets of 2.5 episodes."""
+    import torch
+
+    from lbk8s import LBVecEnv
+    B, K, seed = 4096, 50, 2024
+    env = LBVecEnv(B, seed=seed, as_tensors=True)
+    orc = oracle_mod.OracleBatch({}, B, trace=False, seed=seed)
+    orc.init()
+    np.testing.assert_array_equal(env.reset().cpu().numpy(), orc.reset())
+    R = env.cfg.obs_rows
+    obs = torch.empty((K, B, R, 8), dtype=torch.float32, device="cuda")
+    rew = torch.empty((K, B), dtype=torch.float32, device="cuda")
+    done = torch.empty((K, B), dtype=torch.uint8, device="cuda")
+    for launch in range(5):
+        env.rollout("random", K, obs_out=obs, reward_out=rew, done_out=done)
+        o, r, d = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy().astype(bool)
+        for k in range(K):
+            o2, r2, d2, _, _ = orc.step(orc.policy_random())
+            s = launch * K + k
+            np.testing.assert_array_equal(r[k], r2, err_msg=f"reward step {s}")
+            np.testing.assert_array_equal(d[k], d2, err_msg=f"done step {s}")
+            np.testing.assert_array_equal(o[k], o2, err_msg=f"obs step {s}")
+    assert env.status() == 0
