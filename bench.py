@@ -166,13 +166,19 @@ def main(argv=None):
     from lbk8s import LBVecEnv
     from lbk8s.dist import shard
     from lbk8s.info import ST_EPISODE
-    if torch.cuda.device_count() < world:
-        raise SystemExit(f"bench.py: {world} ranks but {torch.cuda.device_count()} visible GPUs")
-    dev = torch.device("cuda", local)
+    # one GPU per rank over RCCL; LBK8S_DIST_BACKEND=gloo (a test mode) lets ranks share GPUs
+    backend = os.environ.get("LBK8S_DIST_BACKEND", "nccl")
+    ngpu = torch.cuda.device_count()
+    if backend == "nccl" and ngpu < world:
+        raise SystemExit(f"bench.py: {world} ranks but {ngpu} visible GPUs")
+    dev = torch.device("cuda", local % max(ngpu, 1))
     torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     total = args.envs * (world if args.weak else 1)
     off, B = shard(total, rank, world)
     cfg_kwargs = CONFIGS[args.config]
