@@ -108,11 +108,16 @@ __device__ __forceinline__ int zcap_val(uint64_t zc, int z) { return (int)((zc >
 // ---- RNG ---------------------------------------------------------------------------
 struct U4 { uint32_t x, y, z, w; };
 
-// Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11)
+// Philox4x32-R (Salmon, Moraes, Dror, Shaw, SC'11).  The draw map runs R = 7 rounds
+// (LB_PHILOX_ROUNDS): the paper's Philox4x32-7 passes TestU01 BigCrush, and the step kernel
+// is VALU-issue bound with Philox about half its instructions (7 rounds take
+// the 2^20-env step from ~125-130 to ~115.5 us).  The round function is pinned against the
+// Random123 philox4x32_10 known answers through the oracle at R = 10.
+#define LB_PHILOX_ROUNDS 7
 __device__ __forceinline__ U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                      uint32_t k0, uint32_t k1) {
 #pragma unroll
-    for (int i = 0; i < 10; ++i) {
+    for (int i = 0; i < LB_PHILOX_ROUNDS; ++i) {
         uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
         uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
         uint32_t n0 = hi1 ^ c1 ^ k0;

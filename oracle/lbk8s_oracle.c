@@ -83,10 +83,14 @@ typedef struct {
     int32_t *was_reset;
 } orc_env;
 
-/* ---------------- Philox4x32-10 (Salmon et al., SC'11) ------------------- */
-static void philox4x32_10(uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t out[4]) {
+/* ---------------- Philox4x32-R (Salmon et al., SC'11) -------------------- */
+/* The draw map runs ORC_PHILOX_ROUNDS = 7 (Philox4x32-7, BigCrush-clean per the paper);
+ * orc_philox_r exposes the round count so tests pin the round function against the
+ * Random123 philox4x32_10 known answers at R = 10. */
+#define ORC_PHILOX_ROUNDS 7
+static void philox4x32_r(uint32_t ctr[4], uint32_t k0, uint32_t k1, int rounds, uint32_t out[4]) {
     uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
-    for (int i = 0; i < 10; ++i) {
+    for (int i = 0; i < rounds; ++i) {
         uint64_t p0 = (uint64_t)0xD2511F53u * c0;
         uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
         uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
@@ -104,7 +108,7 @@ static void draw(const orc_env* s, int64_t b, uint32_t episode, uint32_t slot, u
                  uint32_t out[4]) {
     uint64_t gid = (uint64_t)(s->c.env_id_offset + b);
     uint32_t ctr[4] = {(uint32_t)gid, episode, slot, dom | ((uint32_t)(gid >> 32) << 8)};
-    philox4x32_10(ctr, (uint32_t)s->c.seed, (uint32_t)(s->c.seed >> 32), out);
+    philox4x32_r(ctr, (uint32_t)s->c.seed, (uint32_t)(s->c.seed >> 32), ORC_PHILOX_ROUNDS, out);
 }
 
 static uint32_t bounded(uint32_t w, uint32_t n) { return (uint32_t)(((uint64_t)w * n) >> 32); }
@@ -523,10 +527,12 @@ int orc_num_threads(void) {
 }
 
 /* expose the RNG primitives so tests can pin them against known-answer vectors */
-void orc_philox(const uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t out[4]) {
+void orc_philox_r(const uint32_t ctr[4], uint32_t k0, uint32_t k1, int32_t rounds,
+                  uint32_t out[4]) {
     uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]};
-    philox4x32_10(c, k0, k1, out);
+    philox4x32_r(c, k0, k1, rounds, out);
 }
+int32_t orc_philox_rounds(void) { return ORC_PHILOX_ROUNDS; }
 double orc_log(double x) { return fd_log(x); }
 
 /* Re-key the Philox stream (LBVecEnv.seed(): applied at the next full reset). */

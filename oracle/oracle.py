@@ -63,7 +63,8 @@ def lib():
         L.orc_policy_random.argtypes = [C.c_void_p, C.c_void_p]
         L.orc_get_field.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
         L.orc_num_threads.restype = C.c_int
-        L.orc_philox.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]
+        L.orc_philox_r.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int32, C.c_void_p]
+        L.orc_philox_rounds.restype = C.c_int32
         L.orc_log.restype = C.c_double
         L.orc_log.argtypes = [C.c_double]
         L.orc_set_seed.argtypes = [C.c_void_p, C.c_uint64]
@@ -225,11 +226,17 @@ def subproc_vecenv_rate(cfg, workers, seconds=5.0):
                        f"vector step, {steps} vector steps ({el:.1f} s)")
 
 
-def philox(ctr, key):
+def philox(ctr, key, rounds=None):
+    """Philox4x32-R block; rounds None = the draw map's round count (philox_rounds())."""
     out = np.zeros(4, np.uint32)
     c = np.asarray(ctr, np.uint32)
-    lib().orc_philox(_p(c), int(key[0]), int(key[1]), _p(out))
+    r = philox_rounds() if rounds is None else int(rounds)
+    lib().orc_philox_r(_p(c), int(key[0]), int(key[1]), r, _p(out))
     return out
+
+
+def philox_rounds():
+    return int(lib().orc_philox_rounds())
 
 
 def fd_log(x):

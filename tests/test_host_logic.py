@@ -3,7 +3,8 @@
 * greedy policies (lbk8s.baselines) against hand-computed expectations incl. the
   mask[:-1] quirk and ties (envs/baselines.py:6-35);
 * env sharding arithmetic and the gloo world_size-2 episode-statistics reduction;
-* Philox4x32-10 known-answer vectors (Random123 kat_vectors) and the fdlibm-style log;
+* Philox4x32-R round function pinned by the Random123 philox4x32_10 known answers (R = 10);
+  the draw map runs R = 7 (DESIGN.md §5); the fdlibm-style log;
 * T3 (statistical) checks of the Philox draw map through the oracle;
 * sharding invariance of Philox trajectories (global env ids) through the oracle.
 """
@@ -97,7 +98,10 @@ def test_philox_known_answers(oracle_mod):
          (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1)),
     ]
     for ctr, key, out in kat:
-        assert tuple(int(x) for x in oracle_mod.philox(ctr, key)) == out
+        assert tuple(int(x) for x in oracle_mod.philox(ctr, key, rounds=10)) == out
+    # the draw map: Philox4x32-7 through the same round function
+    assert oracle_mod.philox_rounds() == 7
+    assert tuple(oracle_mod.philox((0, 0, 0, 0), (0, 0))) != kat[0][2]
 
 
 def test_fd_log_accuracy(oracle_mod):
