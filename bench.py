@@ -283,7 +283,7 @@ def main(argv=None):
                    "parallelism": f"env-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": ("k_step_tpe + k_reset_listed (lb_step)" if env.cfg.num_endpoints <= 8
+                     "kernel": ("k_step_tpe (lb_step, auto-reset inside)" if env.cfg.num_endpoints <= 8
                                 else "k_step_slice (lb_step)"),
                      "kernel_ms": kernel_ms, "bytes_per_env_step": b_alg, "envs_per_launch": B},
     }

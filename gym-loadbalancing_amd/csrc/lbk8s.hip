@@ -269,7 +269,7 @@ uint64_t align_up(uint64_t x) { return (x + 255) & ~(uint64_t)255; }
 
 struct Offsets {
     uint64_t lat_lut, cpu_lut, lat0, emeta, edyn, t, sc, topo, zcap, nzone, acc2, acc3, sum_lat,
-        sum_cpu, total, last_r, rs_cnt, rs_ids, end;
+        sum_cpu, total, last_r, end;
 };
 
 Offsets offsets(const lb_config* c, int64_t B) {
@@ -294,10 +294,6 @@ Offsets offsets(const lb_config* c, int64_t B) {
     o.sum_cpu = take(B * 8);
     o.total = take(B * 8);
     o.last_r = take(B * 8);
-    // deferred auto-reset lists of the thread-per-env step (k_step_tpe -> k_reset_listed)
-    const uint64_t nseg = g.tpe ? ((uint64_t)B + 63) / 64 : 0;
-    o.rs_cnt = take(nseg * 4);
-    o.rs_ids = take(nseg * 64 * 4);
     o.end = x;
     return o;
 }
@@ -359,8 +355,6 @@ Params make_params(void* state, const lb_config* c, int64_t B) {
     p.sum_cpu = (double*)(base + o.sum_cpu);
     p.total = (double*)(base + o.total);
     p.last_r = (double*)(base + o.last_r);
-    p.rs_cnt = (uint32_t*)(base + o.rs_cnt);
-    p.rs_ids = (uint32_t*)(base + o.rs_ids);
     p.B = B;
     p.env_id_offset = c->env_id_offset;
     p.es = g.tpe ? B : 1;
@@ -517,7 +511,8 @@ int lb_step(void* state, const lb_config* cfg, int64_t num_envs, const int32_t* 
     Geo g = geometry(cfg, num_envs);
     hipStream_t s = (hipStream_t)stream;
     if (g.tpe) {
-        const bool recompute = num_envs >= SCEN_RECOMPUTE_MIN_B;
+        // auto-reset (the finishing envs' reset()) runs inside k_step_tpe
+        const bool recompute = !tr && num_envs >= SCEN_RECOMPUTE_MIN_B;
         if (num_envs <= SMALL_TPE_MAX_B && !recompute) {
             const unsigned nb = (unsigned)((num_envs + 63) / 64);
             if (tr) hipLaunchKernelGGL((k_step_tpe<true, false, 64>), dim3(nb), dim3(64), 0, s, p);
@@ -529,12 +524,6 @@ int lb_step(void* state, const lb_config* cfg, int64_t num_envs, const int32_t* 
         } else {
             hipLaunchKernelGGL((k_step_tpe<false, false>), dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p);
         }
-        if (int r = check_launch()) return r;
-        if (!cfg->auto_reset) return 0;
-        // the deferred reset() of the envs that finished (lists written by the step)
-        const unsigned nb = (unsigned)((num_envs + 64 * RS_SEG - 1) / (64 * RS_SEG));
-        if (tr) hipLaunchKernelGGL(k_reset_listed<true>, dim3(nb), dim3(BLOCK), 0, s, p);
-        else hipLaunchKernelGGL(k_reset_listed<false>, dim3(nb), dim3(BLOCK), 0, s, p);
         return check_launch();
     }
     LB_DISPATCH_SLICE(g.W, g.EPL, {

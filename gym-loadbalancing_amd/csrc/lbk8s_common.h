@@ -179,8 +179,6 @@ struct Params {
     double* sum_cpu;   // [B]
     double* total;     // [B]
     double* last_r;    // [B]
-    uint32_t* rs_cnt;  // thread-per-env layout: finished envs per 64-env wave   [ceil(B/64)]
-    uint32_t* rs_ids;  //                        their env ids, wave w at [64 w]  [64 ceil(B/64)]
     int64_t B, env_id_offset, es, ee;
     int E, Z, N, L, R, EP, NZW, A;
     int reward_fn, rejection, auto_reset;

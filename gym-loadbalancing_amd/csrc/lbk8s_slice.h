@@ -323,42 +323,8 @@ __global__ __launch_bounds__(BLOCK) void k_reset_slice(Params p) {
     if (lane == 0) slice_store_scalars<EPL>(p, env, v);
 }
 
-// Deferred auto-reset of the thread-per-env step (k_step_tpe): reset() of the envs that
-// finished, read from the step's per-wave lists, with RS_W lanes per env (the 24+ node
-// draws spread over lanes instead of one lane's serial chain).  Block b takes the lists of
-// waves RS_SEG b .. RS_SEG (b + 1) - 1 (256 envs: the envs of step block b, so with the
-// same block -> XCD order the lists and the env state it reads are in that XCD's L2);
-// slice s of its 32 slices resets their items s, s + 32, ...  With 1% of the envs
-// finishing per step (staggered episodes) a block has ~3 items: one round of slices.
-// Measured at 2^17 envs: 27.6-28.4 -> 26.9 us per step (8 wave lists per block before).
-// Any state layout: endpoint stores go through eidx.
-constexpr int RS_W = 8, RS_SEG = 4;
-template <bool TRACE>
-__global__ __launch_bounds__(BLOCK) void k_reset_listed(Params p) {
-    constexpr int NS = BLOCK / RS_W;
-    const int lane = threadIdx.x % RS_W, slot = threadIdx.x / RS_W;
-    const int64_t nseg = (p.B + 63) / 64, seg0 = (int64_t)blockIdx.x * RS_SEG;
-    int pre[RS_SEG + 1];
-    pre[0] = 0;
-#pragma unroll
-    for (int k = 0; k < RS_SEG; ++k) pre[k + 1] = pre[k] + (seg0 + k < nseg ? (int)p.rs_cnt[seg0 + k] : 0);
-    for (int i = slot; i < pre[RS_SEG]; i += NS) {
-        int k = 0;
-#pragma unroll
-        for (int q = 1; q < RS_SEG; ++q) k += i >= pre[q];
-        int base = pre[0];
-#pragma unroll
-        for (int q = 1; q < RS_SEG; ++q) base = k == q ? pre[q] : base;
-        const int64_t env = p.rs_ids[(seg0 + k) * 64 + (i - base)];
-        SEnv<1> v;
-        v.t = p.t[env];
-        v.acc3 = p.acc3[env];
-        v.s = sc_unpack(p.sc[env]);
-        slice_reset<RS_W, 1, TRACE>(p, env, lane, v);
-        if (p.obs) slice_write_obs<RS_W, 1>(p, p.obs, env, lane, v);
-        if (lane == 0) slice_store_scalars<1>(p, env, v);
-    }
-}
+// lanes per env of the thread-per-env step's auto-reset (k_step_tpe, lbk8s_tpe.h)
+constexpr int RS_W = 8;
 
 // One step() (:403-513) of the slice's env held in registers, fused with next_request(),
 // get_state(), reward, done and auto-reset: action a in, obs / reward / done of this step

@@ -14,6 +14,7 @@
 #pragma once
 
 #include "lbk8s_common.h"
+#include "lbk8s_slice.h"
 
 namespace lbk {
 
@@ -268,13 +269,25 @@ __global__ __launch_bounds__(NB) void k_reset_tpe(Params p) {
     if (p.obs) tpe_copy_out(p, p.obs, img, env0, COPY_FLAGGED);
 }
 
+// The LDS image and the copy-out are wave-local: a wave orders its own LDS accesses, so it
+// needs no block barrier (which would also wait for every global store the wave has in
+// flight); the compiler is kept from moving LDS accesses across the point.
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// LDS-only block barrier: the waves' global stores stay in flight.
+__device__ __forceinline__ void block_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // step() (:403-513) fused with next_request(), get_state(), reward and done.  RECOMPUTE
 // (Philox mode, many envs): the scenario is redrawn instead of loaded.
-// VecEnv auto-reset: an env whose episode ends gets its terminal obs and episode-stats row
-// here; its reset() is deferred to k_reset_listed (lbk8s_slice.h), which runs next on the
-// stream over the compacted list of those envs (per wave: rs_cnt[wave] ids at
-// rs_ids[64 wave ..]).  Resetting inline made every wave holding one finishing env (~half
-// of them when episodes are staggered) carry reset()'s ~36 serial Philox blocks.
+// VecEnv auto-reset: an env whose episode ends gets its terminal obs and episode-stats row,
+// then its reset() in this kernel with RS_W = 8 lanes (the node draws spread over the
+// lanes instead of one lane's ~36 serial Philox blocks): each wave lists its finishing envs
+// (id, t, acc3, sc) in its own LDS image once the copy-out has read it, and after one
+// LDS-only block barrier the block's waves take the block's list 8 envs per wave-round.
+// The step skips the state stores the reset rewrites (scalars, history counters).
+// Measured against a separate reset kernel over per-wave lists (round 2, bench workload,
+// profiles/r01_ablation.jsonl): 131,072 envs 25.4 -> 23.9 us per step, 2^19 67 -> 64.5,
+// 2^20 equal (112 us): the second launch's ramp, not the reset work, was the cost.
+constexpr int RS_LIST_W = 7;  // words per list item: env, t (2), acc3 (2), sc (2)
 template <bool TRACE, bool RECOMPUTE, int NB = BLOCK>
 __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
     __shared__ uint32_t lds[NB * TPE_CW];
@@ -326,6 +339,9 @@ __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
 
     // ---- phase 1: decode the action, pick the selected endpoint, table lookups
     v.s.step = v.s.step < 0xFFFF ? v.s.step + 1 : 0xFFFF;
+    const bool done = live && v.s.step == p.L;  // (:472)
+    const bool do_reset = done && p.auto_reset;
+    const bool keep = live && !do_reset;  // the state stores reset() below does not redo
     const bool accept = a >= -E && a < E;
     const bool reject = a == E;
     if (a < -E) v.s.bad = 1;  // reference: IndexError; here: treated as unrecognised
@@ -389,7 +405,7 @@ __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
         // decrease in next_request() (:1137-1143) -> the history counters advance
         const uint32_t edA_new = ((oA == ai ? (uint32_t)Mn : (uint32_t)ed_M(edA)) << 20) |
                                  ((uint32_t)Mn << 10) | (uint32_t)jn;
-        if (live) {
+        if (keep) {
             if (oA != ai) *(p.edyn + (int64_t)oA * p.B + env) = ((edO & ~(0x3FFu << 20)) | ((uint32_t)Mn << 20));
             *(p.edyn + (int64_t)ai * p.B + env) = (edA_new);
         }
@@ -424,29 +440,58 @@ __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
             v.s.rz = zo;
         }
     }
-    const bool done = live && v.s.step == p.L;  // (:472)
     if (live) {
         if (p.reward) *(p.reward + env) = ((float)reward);
         if (p.done) p.done[env] = (uint8_t)done;
     }
-    const bool do_reset = done && p.auto_reset;
     tpe_image_env(me, v, do_reset ? TPE_FLAG : 0);
 
-    // ---- VecEnv auto-reset: terminal obs + episode stats; reset() itself is deferred
-    if (p.auto_reset) {
-        const uint64_t m = __ballot(do_reset);
-        if (do_reset) {
-            p.rs_ids[env0 + __popcll(m & ((1ull << lane) - 1))] = (uint32_t)env;
-            if (p.ep_stats)
-                write_stats_row(p, p.ep_stats + env * LB_ST_K, v.s, v.acc2, v.acc3, v.total, v.sum_lat, v.sum_cpu);
-        }
-        if (lane == 0) p.rs_cnt[env0 >> 6] = (uint32_t)__popcll(m);
-    }
-    if (live) tpe_store_scalars(p, env, v);
-    __syncthreads();
-    if (p.term_obs && __syncthreads_or(do_reset)) tpe_copy_out(p, p.term_obs, img, env0, COPY_FLAGGED);
-    // finished envs' post-reset obs come from k_reset_listed
+    // ---- VecEnv auto-reset: terminal obs + episode stats, then reset() below
+    const uint64_t m = __ballot(do_reset);
+    if (do_reset && p.ep_stats)
+        write_stats_row(p, p.ep_stats + env * LB_ST_K, v.s, v.acc2, v.acc3, v.total, v.sum_lat, v.sum_cpu);
+    if (keep) tpe_store_scalars(p, env, v);
+    wave_lds_sync();
+    if (p.term_obs && m) tpe_copy_out(p, p.term_obs, img, env0, COPY_FLAGGED);
+    // finished envs' post-reset obs come from their reset()
     if (p.obs) tpe_copy_out(p, p.obs, img, env0, p.auto_reset ? COPY_UNFLAGGED : COPY_ALL);
+    if (p.auto_reset) {  // uniform over the grid: every wave reaches the barrier
+        constexpr int NW = NB / 64;
+        wave_lds_sync();
+        if (do_reset) {  // the wave's list replaces its (copied-out) image
+            uint32_t* it = img + 1 + RS_LIST_W * __popcll(m & ((1ull << lane) - 1));
+            const uint64_t tb = (uint64_t)__double_as_longlong(v.t), sc = sc_pack(v.s);
+            it[0] = (uint32_t)env;
+            it[1] = (uint32_t)tb; it[2] = (uint32_t)(tb >> 32);
+            it[3] = (uint32_t)v.acc3; it[4] = (uint32_t)(v.acc3 >> 32);
+            it[5] = (uint32_t)sc; it[6] = (uint32_t)(sc >> 32);
+        }
+        if (lane == 0) img[0] = (uint32_t)__popcll(m);
+        if (NW > 1) block_lds_sync();
+        else wave_lds_sync();
+        int pre[NW + 1];
+        pre[0] = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) pre[w + 1] = pre[w] + (int)lds[w * 64 * TPE_CW];
+        const int wv = threadIdx.x >> 6, g = lane / RS_W, gl = lane % RS_W;
+        for (int i = wv * (64 / RS_W) + g; i < pre[NW]; i += NW * (64 / RS_W)) {
+            int q = 0;
+#pragma unroll
+            for (int w = 1; w < NW; ++w) q += i >= pre[w];
+            int base = 0;
+#pragma unroll
+            for (int w = 1; w < NW; ++w) base = q == w ? pre[w] : base;
+            const uint32_t* it = lds + q * 64 * TPE_CW + 1 + RS_LIST_W * (i - base);
+            const int64_t renv = (int64_t)it[0];
+            SEnv<1> sv;
+            sv.t = __longlong_as_double((long long)((uint64_t)it[1] | ((uint64_t)it[2] << 32)));
+            sv.acc3 = (uint64_t)it[3] | ((uint64_t)it[4] << 32);
+            sv.s = sc_unpack((uint64_t)it[5] | ((uint64_t)it[6] << 32));
+            slice_reset<RS_W, 1, TRACE>(p, renv, gl, sv);
+            if (p.obs) slice_write_obs<RS_W, 1>(p, p.obs, renv, gl, sv);
+            if (gl == 0) slice_store_scalars<1>(p, renv, sv);
+        }
+    }
 }
 
 }  // namespace lbk

@@ -200,3 +200,45 @@ def test_config2_rollout_matches_oracle(oracle_mod):
             np.testing.assert_array_equal(d[k], d2, err_msg=f"done step {s}")
             np.testing.assert_array_equal(o[k], o2, err_msg=f"obs step {s}")
     assert env.status() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [4096, 131072, (1 << 19) + 4096])
+def test_staggered_auto_reset_matches_oracle(oracle_mod, B):
+    """Auto-reset with staggered episodes (1/L of the envs end every step, as in bench.py):
+    the finishing envs' reset() inside k_step_tpe (a block's list, 8 lanes per env, after
+    one LDS-only barrier) with 64-thread blocks (4096), 256-thread blocks with the stored
+    scenario (131,072) and with the recomputed one (2^19 + 4096).  Kernels == C oracle bit
+    for bit: obs, reward, done, terminal obs, times, latencies, loads."""
+    import torch
+
+    from lbk8s import LBVecEnv
+    L, seed = 10, 4242
+    cfg = dict(episode_length=L)
+    env = LBVecEnv(B, seed=seed, **cfg)
+    orc = oracle_mod.OracleBatch(cfg, B, trace=False, seed=seed)
+    orc.init()
+    np.testing.assert_array_equal(env.reset(), orc.reset())
+    rng = np.random.default_rng(7)
+    A, E = env.action_space.n, env.cfg.num_endpoints
+    gid = np.arange(B)
+    for r in range(1, L):  # bench.py's stagger: envs with id % L == r restart after step r
+        a = rng.integers(-E, A, size=B).astype(np.int32)
+        env.step(a)
+        orc.step(a)
+        m = (gid % L) == r
+        env.reset_masked(torch.from_numpy(m.astype(np.uint8)))
+        orc.reset(mask=m.astype(np.uint8))
+    for s in range(2 * L + 3):
+        a = rng.integers(-E, A, size=B).astype(np.int32)
+        o1, r1, d1, _ = env.step(a)
+        o2, r2, d2, t2, _ = orc.step(a)
+        assert 0 < d1.sum() < B
+        np.testing.assert_array_equal(r1, r2, err_msg=f"reward step {s}")
+        np.testing.assert_array_equal(d1, d2, err_msg=f"done step {s}")
+        np.testing.assert_array_equal(o1, o2, err_msg=f"obs step {s}")
+        np.testing.assert_array_equal(env.terminal_obs.cpu().numpy()[d1], t2[d1])
+    np.testing.assert_array_equal(env.field("avg_load_served").cpu().numpy(), orc.field("loads"))
+    np.testing.assert_array_equal(env.field("current_time").cpu().numpy(), orc.field("t"))
+    np.testing.assert_array_equal(env.field("endpoint_latency").cpu().numpy(), orc.field("ep_lat"))
+    assert env.status() == 0

@@ -42,7 +42,7 @@ def main():
     # the last 16 launches are the timed-step workload (earlier ones: the stagger setup)
     fetch_raw = statistics.median(f[step][-13:])
     write = statistics.median(w[step][-13:])
-    rs = [k for k in f if "k_reset_listed" in k]
+    rs = [k for k in f if "k_reset_listed" in k]  # builds before the in-step auto-reset
     reset = None
     if rs:
         rf, rw = statistics.median(f[rs[0]][-13:]) * factor, statistics.median(w[rs[0]][-13:])
