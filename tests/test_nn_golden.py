@@ -90,12 +90,20 @@ def test_ppo_minibatch_update_matches_reference(device, golden):
     opt = torch.optim.Adam(agent.parameters(), lr=2.5e-4, eps=1e-5)
     opt.zero_grad()
     loss.backward()
-    # gradients: elementwise, with an absolute floor of 1e-5 x the largest gradient (the
-    # actor's last Gamma has a true gradient of 0: its entries are rounding noise)
+    # gradients: elementwise, with an absolute floor of 1e-5 x the largest gradient.  The
+    # actor's last Gamma has a true gradient of 0 (Gamma max(h) adds the same constant to
+    # every logit of a set, and the log-softmax is shift-invariant): its entries are the
+    # rounding noise of sum_r dlogits, which depends on the host BLAS's summation order, so
+    # both sides are only bounded there (1e-4 x the largest gradient; R = 65's noise reaches
+    # ~2e-5 of it on some CPUs).
     gmax = max(np.abs(d["grad__" + n.replace(".", "__")]).max() for n, _ in agent.named_parameters())
     for n, p in agent.named_parameters():
-        close(p.grad, d["grad__" + n.replace(".", "__")], what="grad " + n, rtol=t["rtol"] * 10,
-              atol=max(t["atol"] * 10, 1e-5 * gmax))
+        exp = d["grad__" + n.replace(".", "__")]
+        if n == "actor.net.4.Gamma.weight":
+            assert np.abs(exp).max() <= 1e-4 * gmax
+            assert float(p.grad.abs().max()) <= 1e-4 * gmax, n
+            continue
+        close(p.grad, exp, what="grad " + n, rtol=t["rtol"] * 10, atol=max(t["atol"] * 10, 1e-5 * gmax))
     gn = torch.nn.utils.clip_grad_norm_(agent.parameters(), 0.5)
     close(gn, d["grad_norm"], what="grad norm", **t)
     opt.step()
