@@ -1,14 +1,20 @@
 #!/usr/bin/env python3
 """Benchmark: vectorized LoadBalancerK8sEnv env-steps/s on MI355X (BASELINE.json config 3).
 
-One bench "step" = one vector step of every env on every GPU: the fused step kernel
-(lb_step: take_action + reward + next_request + get_state + auto-reset) with the env's
-uniform random policy drawn inside the kernel (lb_step with actions == NULL; the random
-policy of BASELINE configs 2/3, the same draws lb_policy(random) returns).  Observations,
-rewards and dones go into a T-deep device ring, the shape of PPO's rollout storage
-(ppo_deepset.py:136-143), so writes stream to HBM instead of sitting in the 256 MB
-Infinity Cache; terminal observations and episode-statistics rows of finished envs are
-written too.  Env state is resident in HBM before timing.
+One bench "step" = one vector step of every env on every GPU: take_action + reward +
+next_request + get_state + auto-reset with the env's uniform random policy drawn on the
+device (the random policy of BASELINE configs 2/3, the same draws lb_policy(random)
+returns).  Observations, rewards and dones go into a T-deep device ring, the shape of PPO's
+rollout storage (ppo_deepset.py:136-143), so writes stream to HBM instead of sitting in the
+256 MB Infinity Cache; terminal observations and episode-statistics rows of finished envs
+are written too.  Env state is resident in HBM before timing.
+
+Two launch shapes run the same steps (bit for bit, tests/test_gpu_api.py):
+  --launch rollout (default): lb_rollout, K = T vector steps per launch (k_rollout_tpe),
+      the env state in registers between the steps of a launch, every step's outputs in
+      its ring slot -- the step-only workload of config 3 (no host policy in the loop);
+  --launch step: one lb_step launch per vector step (k_step_tpe), the VecEnv.step() shape
+      a host/NN policy needs; measured in the same run and reported under "lb_step".
 
 Episodes are staggered before timing (env i starts at step i mod episode_length), so every
 timed step ends and auto-resets 1/episode_length of the envs — the steady state of a
@@ -72,6 +78,9 @@ def parse(argv):
     ap.add_argument("--config", default="default", choices=sorted(CONFIGS))
     ap.add_argument("--ring", type=int, default=16, help="rollout ring depth (obs slots)")
     ap.add_argument("--no-graph", action="store_true", help="launch every step eagerly")
+    ap.add_argument("--launch", default="rollout", choices=("rollout", "step"),
+                    help="rollout: K = ring steps per lb_rollout launch; step: one lb_step per step")
+    ap.add_argument("--no-step-line", action="store_true", help="rollout mode: skip the lb_step measurement")
     ap.add_argument("--lockstep", action="store_true", help="do not stagger episodes (all envs reset together)")
     ap.add_argument("--geometry", default="auto", choices=("auto", "tpe", "slice"), help="E <= 8 kernel shape")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -194,81 +203,103 @@ def main(argv=None):
     def one_step(i):  # actions=None: the env's random policy, drawn inside the step kernel
         env.step_device(None, obs_out=obs_ring[i % T], reward_out=rew_ring[i % T], done_out=done_ring[i % T])
 
+    def one_launch(mode, i, end):  # -> vector steps launched from step i
+        if mode == "step":
+            one_step(i)
+            return 1
+        n = min(T - i % T, end - i)  # K = the ring's remaining slots: T steps per launch
+        env.rollout("random", n, obs_out=obs_ring[i % T], reward_out=rew_ring[i % T], done_out=done_ring[i % T])
+        return n
+
     # setup: stagger the episodes so 1/L of the envs end (and auto-reset) at every step
     env.reset()
     gid = torch.arange(off, off + B, device=dev)
     for r in range(1, 1 if args.lockstep else L):
         one_step(0)
         env.reset_masked((gid % L) == r)
-    # one graph of T steps (ring slots 0..T-1): no host launch cost between the kernels
-    graph = None
-    if not args.no_graph:
-        side = torch.cuda.Stream(dev)
-        side.wait_stream(stream)
-        with torch.cuda.stream(side):
-            one_step(0)
-        stream.wait_stream(side)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            for i in range(T):
-                one_step(i)
 
-    def run(first, count):
-        i, end = first, first + count
-        while i < end:
-            if graph is not None and i % T == 0 and end - i >= T:
-                graph.replay()
-                i += T
-            else:
-                one_step(i)
-                i += 1
+    def measure(mode):
+        # one graph of T steps (ring slots 0..T-1): no host launch cost between the kernels
+        graph = None
+        if not args.no_graph:
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(stream)
+            with torch.cuda.stream(side):
+                one_step(0)
+            stream.wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                i = 0
+                while i < T:
+                    i += one_launch(mode, i, T)
 
-    run(0, args.warmup)
+        def run(first, count):
+            i, end = first, first + count
+            while i < end:
+                if graph is not None and i % T == 0 and end - i >= T:
+                    graph.replay()
+                    i += T
+                else:
+                    i += one_launch(mode, i, end)
+
+        run(0, args.warmup)
+        K = args.steps
+        ep0 = env.stats()[:, ST_EPISODE].sum().item()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        # timed: exactly K steps, barrier + synchronize on both sides; HIP events on the
+        # kernels' stream bracket the same launches (their average = the kernel's duration)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        run(args.warmup, K)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        own_el = el
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        kernel_ms = ev0.elapsed_time(ev1) / K
+        resets = int(env.stats()[:, ST_EPISODE].sum().item() - ep0)
+        assert env.status() == 0, "kernel flagged bad actions / unreset envs"
+        assert kernel_ms <= own_el / K * 1e3 * 1.001, "event window longer than the wall-clock window"
+        if world > 1:
+            v = torch.tensor([float(resets)], dtype=torch.float64, device=dev)
+            dist.all_reduce(v)
+            resets = int(v[0].item())
+        del graph
+        return dict(el=el, kernel_ms=kernel_ms, resets=resets, graphs=not args.no_graph)
+
     K = args.steps
-    ep0 = env.stats()[:, ST_EPISODE].sum().item()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    # timed: exactly K steps, barrier + synchronize on both sides; HIP events on the step
-    # kernels' stream bracket the same K launches (their average = the kernel's duration)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    run(args.warmup, K)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    own_el = el
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    kernel_ms = ev0.elapsed_time(ev1) / K
-    resets = int(env.stats()[:, ST_EPISODE].sum().item() - ep0)
-    assert env.status() == 0, "kernel flagged bad actions / unreset envs"
-    assert kernel_ms <= own_el / K * 1e3 * 1.001, "event window longer than the wall-clock window"
-    if world > 1:
-        v = torch.tensor([float(resets), float(B)], dtype=torch.float64, device=dev)
-        dist.all_reduce(v)
-        resets = int(v[0].item())
-
+    res = measure(args.launch)
+    step_res = measure("step") if args.launch == "rollout" and not args.no_step_line else None
+    el, kernel_ms, resets = res["el"], res["kernel_ms"], res["resets"]
     value = total * K / el
-    b_alg = algorithmic_bytes(env.cfg, reads_actions=False)
+    b_step = algorithmic_bytes(env.cfg, reads_actions=False)
+    out_b = 32 * R + 5  # obs rows + reward + done, written every step
+    # a rollout launch reads and writes the state once for its T steps
+    b_alg = b_step if args.launch == "step" else out_b + (b_step - out_b) / T
     achieved = b_alg * B / (kernel_ms * 1e-3) / 1e9
     traffic = None
+    pmc_path = args.pmc_json if args.launch == "step" else args.pmc_json.replace(".json", "_rollout.json")
     try:
-        with open(args.pmc_json) as f:
+        with open(pmc_path) as f:
             pmc = json.load(f)
         if pmc.get("config") == args.config and pmc.get("envs") == B:
-            # one bench step = the step kernel + the deferred-reset kernel (both inside the
-            # event window that kernel_ms comes from)
-            traffic = pmc.get("hbm_bytes_per_launch")
-            if traffic is not None and pmc.get("reset_kernel"):
-                traffic += pmc["reset_kernel"]["hbm_bytes_per_launch"]
+            traffic = pmc.get("hbm_bytes_per_launch")  # per launch: T steps in rollout mode
     except (OSError, ValueError):
         pass
+    tpe = env.cfg.num_endpoints <= 8 and (args.geometry == "tpe" or (args.geometry == "auto" and B >= 32768))
+    if args.launch == "step":
+        kname = "k_step_tpe (lb_step, auto-reset inside)" if tpe else "k_step_slice (lb_step)"
+    else:
+        kname = (f"k_rollout_tpe (lb_rollout, {T} steps per launch, random policy, auto-reset inside)" if tpe
+                 else f"k_rollout_slice (lb_rollout, {T} steps per launch)")
     line = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": K,
         "warmup": args.warmup, "ms_per_step": el / K * 1e3, "higher_is_better": True,
@@ -277,16 +308,24 @@ def main(argv=None):
         "config": {"workload": f"config 3: {total} {args.config}-scenario envs in total "
                                f"(E={env.cfg.num_endpoints}, N={env.cfg.num_nodes}, Z={env.cfg.num_zones}, "
                                f"{env.cfg.reward_function}), {B} per GPU, obs ring T={T}, "
-                               + ("lockstep" if args.lockstep else "staggered") + " episodes",
+                               + ("lockstep" if args.lockstep else "staggered") + " episodes, "
+                               + (f"{T} vector steps per lb_rollout launch" if args.launch == "rollout"
+                                  else "one lb_step launch per vector step"),
                    "envs_per_gpu": B, "total_envs": total, "scenario": args.config, "episode_length": L,
-                   "resets_in_window": resets, "graphs": graph is not None, "geometry": args.geometry,
-                   "parallelism": f"env-sharded x{world}"},
+                   "resets_in_window": resets, "graphs": res["graphs"], "geometry": args.geometry,
+                   "launch": args.launch, "parallelism": f"env-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": ("k_step_tpe (lb_step, auto-reset inside)" if env.cfg.num_endpoints <= 8
-                                else "k_step_slice (lb_step)"),
-                     "kernel_ms": kernel_ms, "bytes_per_env_step": b_alg, "envs_per_launch": B},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
+                     "kernel_ms": kernel_ms, "bytes_per_env_step": b_alg, "envs_per_launch": B,
+                     "steps_per_launch": T if args.launch == "rollout" else 1},
     }
+    if step_res is not None:
+        ks = step_res["kernel_ms"]
+        line["lb_step"] = {"value": total * K / step_res["el"], "ms_per_step": step_res["el"] / K * 1e3,
+                           "kernel_ms": ks, "bytes_per_env_step": b_step,
+                           "frac": b_step * B / (ks * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                           "kernel": "k_step_tpe (lb_step, auto-reset inside)" if tpe else "k_step_slice (lb_step)",
+                           "resets_in_window": step_res["resets"]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(cfg_kwargs, args.cpu_seconds)
     if rank == 0:

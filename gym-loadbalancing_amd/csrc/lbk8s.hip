@@ -269,7 +269,7 @@ uint64_t align_up(uint64_t x) { return (x + 255) & ~(uint64_t)255; }
 
 struct Offsets {
     uint64_t lat_lut, cpu_lut, lat0, emeta, edyn, t, sc, topo, zcap, nzone, acc2, acc3, sum_lat,
-        sum_cpu, total, last_r, end;
+        sum_cpu, total, last_r, rec, end;
 };
 
 Offsets offsets(const lb_config* c, int64_t B) {
@@ -294,6 +294,8 @@ Offsets offsets(const lb_config* c, int64_t B) {
     o.sum_cpu = take(B * 8);
     o.total = take(B * 8);
     o.last_r = take(B * 8);
+    // thread-per-env layout: k_rollout_tpe's next-episode records (scratch, per launch)
+    o.rec = take(g.tpe ? (uint64_t)B * RO_REC_BYTES : 0);
     o.end = x;
     return o;
 }
@@ -355,6 +357,7 @@ Params make_params(void* state, const lb_config* c, int64_t B) {
     p.sum_cpu = (double*)(base + o.sum_cpu);
     p.total = (double*)(base + o.total);
     p.last_r = (double*)(base + o.last_r);
+    p.rec = g.tpe ? (uint4*)(base + o.rec) : nullptr;
     p.B = B;
     p.env_id_offset = c->env_id_offset;
     p.es = g.tpe ? B : 1;
@@ -544,7 +547,34 @@ int lb_rollout(void* state, const lb_config* cfg, int64_t num_envs, int32_t poli
     if (steps < 0) return fail("steps must be >= 0");
     Geo g = geometry(cfg, num_envs);
     hipStream_t s = (hipStream_t)stream;
-    if (g.tpe) {  // thread-per-env layout: K policy + step launches
+    if (g.tpe && g.NZW <= 2) {  // thread-per-env layout, N <= 64: K steps in one launch
+        Params p = make_params(state, cfg, num_envs);
+        p.obs = obs_out;
+        p.reward = reward_out;
+        p.done = done_out;
+        p.term_obs = terminal_obs_out;
+        p.ep_stats = ep_stats_out;
+        const bool small = num_envs <= SMALL_TPE_MAX_B;
+        const dim3 grid(small ? (unsigned)((num_envs + 63) / 64) : env_blocks(num_envs)), block(small ? 64 : BLOCK);
+        // episodes longer than the launch: next episodes drawn before the first step
+        const bool pre = cfg->auto_reset && cfg->episode_length > steps;
+#define LB_ROLLOUT_TPE_NB(NB_, KIND_)                                                                         \
+        if (pre) hipLaunchKernelGGL((k_rollout_tpe<NB_, KIND_, true>), grid, block, 0, s, p, (int)steps, actions_out); \
+        else hipLaunchKernelGGL((k_rollout_tpe<NB_, KIND_, false>), grid, block, 0, s, p, (int)steps, actions_out);
+#define LB_ROLLOUT_TPE(KIND_)                         \
+        if (small) { LB_ROLLOUT_TPE_NB(64, KIND_) }   \
+        else { LB_ROLLOUT_TPE_NB(BLOCK, KIND_) }
+        switch (policy) {
+        case LB_POLICY_TOPOLOGY_GREEDY: LB_ROLLOUT_TPE(LB_POLICY_TOPOLOGY_GREEDY); break;
+        case LB_POLICY_ZONE_CPU_GREEDY: LB_ROLLOUT_TPE(LB_POLICY_ZONE_CPU_GREEDY); break;
+        case LB_POLICY_ENDPOINT_CPU_GREEDY: LB_ROLLOUT_TPE(LB_POLICY_ENDPOINT_CPU_GREEDY); break;
+        default: LB_ROLLOUT_TPE(LB_POLICY_RANDOM); break;
+        }
+#undef LB_ROLLOUT_TPE
+#undef LB_ROLLOUT_TPE_NB
+        return check_launch();
+    }
+    if (g.tpe) {  // thread-per-env layout, N > 64: K policy + step launches
         if (policy != LB_POLICY_RANDOM && !actions_out)
             return fail("lb_rollout on the thread-per-env layout needs actions_out for a greedy policy");
         const int64_t R = cfg->num_endpoints + (cfg->rejection_allowed ? 1 : 0);

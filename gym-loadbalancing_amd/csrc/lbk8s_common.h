@@ -36,6 +36,7 @@ constexpr int CPU_ROWS = 128;     // initial node cpu in [0, 127]
 constexpr int NZW_MAX = 8;        // node-zone words of 32 nodes -> num_nodes <= 256
 constexpr int EMAX = 256;
 constexpr int TPE_E = 8;          // thread-per-env path: E <= 8 endpoints in registers
+constexpr int RO_REC_BYTES = 160; // k_rollout_tpe's next-episode record per env (lbk8s_tpe.h)
 
 // Philox domains — the framework's draw map; restated by the oracle.
 enum : uint32_t { D_INIT = 1, D_NODE = 2, D_EP = 3, D_TOPO = 4, D_REQ_X = 5, D_REQ_I = 6,
@@ -179,6 +180,7 @@ struct Params {
     double* sum_cpu;   // [B]
     double* total;     // [B]
     double* last_r;    // [B]
+    uint4* rec;        // [B][RO_REC_BYTES / 16] next-episode records (thread-per-env rollout scratch)
     int64_t B, env_id_offset, es, ee;
     int E, Z, N, L, R, EP, NZW, A;
     int reward_fn, rejection, auto_reset;

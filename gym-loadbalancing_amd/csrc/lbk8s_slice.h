@@ -207,8 +207,9 @@ __device__ __forceinline__ void slice_next_request(const Params& p, int64_t env,
     v.s.rz = (int)((word >> (2 * (n & 31))) & 3);
 }
 
-// reset() (:290-400) into registers, then the per-episode state stores.
-template <int W, int EPL, bool TRACE>
+// reset() (:290-400) into registers, then the per-episode state stores (STORE = false: a
+// multi-step kernel that keeps the env in registers writes it back itself).
+template <int W, int EPL, bool TRACE, bool STORE = true>
 __device__ __forceinline__ void slice_reset(const Params& p, int64_t env, int lane, SEnv<EPL>& v) {
     const uint32_t episode = (uint32_t)(v.acc3 >> 32) + 1;
     // nodes (:349-373): zone capacity and the 2-bit zone of every node, one 32-node word
@@ -225,7 +226,7 @@ __device__ __forceinline__ void slice_reset(const Params& p, int64_t env, int la
         word = slice_or64<W>(word);
         if (w == 0) v.nz0 = word;
         if (w == 1) v.nz1 = word;
-        if (lane == 0) p.nzone[w * p.B + env] = word;
+        if (STORE && lane == 0) p.nzone[w * p.B + env] = word;
     }
     if (p.NZW < 2) v.nz1 = 0;
     zc = slice_sum64<W>(zc);
@@ -271,7 +272,7 @@ __device__ __forceinline__ void slice_reset(const Params& p, int64_t env, int la
             v.olat[k] = (float)v.lat0[k];
             v.ocpu[k] = (float)cpu;
         }
-        if (e < p.EP) {  // (the thread-per-env layout has no padding slots: EP = E)
+        if (STORE && e < p.EP) {  // (the thread-per-env layout has no padding slots: EP = E)
             const int64_t i = eidx(p, env, e);
             p.lat0[i] = v.lat0[k];
             p.emeta[i] = v.em[k];
@@ -302,7 +303,7 @@ __device__ __forceinline__ void slice_reset(const Params& p, int64_t env, int la
     v.last_r = p.init_last_r;
     v.s.step = 0; v.s.acc = 0; v.s.intra = 0; v.s.penalty = 0; v.s.reset_done = 1;
     slice_next_request<W, TRACE, EPL>(p, env, lane, true, v);
-    if (lane == 0) {
+    if (STORE && lane == 0) {
         p.topo[env] = topo;
         p.zcap[env] = zc;
     }

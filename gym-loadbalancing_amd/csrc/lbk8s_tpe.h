@@ -276,6 +276,144 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcn
 // LDS-only block barrier: the waves' global stores stay in flight.
 __device__ __forceinline__ void block_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// step() (:403-513) after the step counter advanced, for this lane's env held in registers:
+// action decode, table lookups, take_action (:578-686), reward (:516-567), next_request()
+// (:1131-1163).  Writes the endpoint words of the env's obs image (me) and returns the
+// reward.  ED_REGS: the history counters advance in ed[] (the multi-step rollout keeps them
+// in registers); otherwise the changed words are stored at once when keep is set.
+// STORED: the request node's zone comes from the node-zone words (nodes >= 64 from HBM)
+// instead of a redraw.
+// ED_REGS also keeps the observed latency / cpu of every endpoint in olat / ocpu (float32,
+// the obs columns): only the selected endpoint's change in a step, so the rollout gathers 4
+// table values per step instead of up to 2E + 4.
+template <bool TRACE, bool STORED, bool ED_REGS>
+__device__ __forceinline__ double tpe_step_core(const Params& p, int64_t ev, int64_t env, bool keep, TEnv& v,
+                                                const double (&lat0)[TPE_E], const uint32_t (&em)[TPE_E],
+                                                uint32_t (&ed)[TPE_E], float (&olat)[TPE_E], float (&ocpu)[TPE_E],
+                                                int a, uint32_t* me) {
+    constexpr bool stored = STORED;
+    const int E = p.E;
+    const bool accept = a >= -E && a < E;
+    const bool reject = a == E;
+    if (a < -E) v.s.bad = 1;  // reference: IndexError; here: treated as unrecognised
+    if (!v.s.reset_done) v.s.bad = 1;
+    const int ai = accept ? (a < 0 ? a + E : a) : 0;
+    uint32_t emA = em[0], edA = ed[0];
+    double lat0A = lat0[0];
+#pragma unroll
+    for (int e = 1; e < TPE_E; ++e)
+        if (ai == e) { emA = em[e]; edA = ed[e]; lat0A = lat0[e]; }
+    const int oA = em_owner(emA);
+    uint32_t edO = ed[0];
+#pragma unroll
+    for (int e = 1; e < TPE_E; ++e)
+        if (oA == e) edO = ed[e];
+    const int jA = ed_j(edA);
+    const int Mn = ed_M(edO) < CMAX ? ed_M(edO) + 1 : CMAX;
+    const int jn = jA < CMAX ? jA + 1 : CMAX;
+    const int k0A = (int)lat0A, c0A = em_c0(emA);
+    const double lut_selA = p.lat_lut[(jA) * LAT_ROWS + k0A];
+    const double sel_cpu = p.cpu_lut[(ed_m(edA)) * CPU_ROWS + c0A];
+    const double next_lat = p.lat_lut[(jn) * LAT_ROWS + k0A];
+    const double next_cpu = p.cpu_lut[(Mn) * CPU_ROWS + c0A];
+    int cnt = 0;  // #{e != ai : loads[e] <= loads[ai]} for the O(E) Gini update
+#pragma unroll
+    for (int e = 0; e < TPE_E; ++e) {
+        if (e < E) {
+            const int j = ed_j(ed[e]);
+            // table rows 0 are the initial values: only endpoints selected (j > 0) /
+            // refreshed (m > 0) this episode gather from the LUTs
+            float ol, oc;
+            if constexpr (ED_REGS) {
+                ol = olat[e];
+                oc = ocpu[e];
+            } else {
+                const int m = ed_m(ed[e]);
+                double l = lat0[e], c = (double)em_c0(em[e]);
+                if (j) l = p.lat_lut[j * LAT_ROWS + (int)lat0[e]];
+                if (m) c = p.cpu_lut[m * CPU_ROWS + em_c0(em[e])];
+                ol = (float)l;
+                oc = (float)c;
+            }
+            if (accept && e == ai) { ol = (float)next_lat; oc = (float)next_cpu; }
+            if constexpr (ED_REGS) {  // (the caller writes the obs rows from olat / ocpu)
+                olat[e] = ol;
+                ocpu[e] = oc;
+            } else {
+                const int z = em_zone(em[e]);
+                me[4 + 3 * e] = (uint32_t)z | ((uint32_t)zcap_val(v.zcap, z) << 2);
+                me[5 + 3 * e] = __float_as_uint(oc);
+                me[6 + 3 * e] = __float_as_uint(ol);
+            }
+            if (e != ai && j <= jA) ++cnt;
+        }
+    }
+
+    // ---- take_action (:578-686)
+    double reward;
+    if (accept) {
+        const int zA = em_zone(emA);
+        const double sel_lat = jA == 0 ? lat0A : lut_selA;
+        const int tl = topo_val(v.topo, v.s.rz, zA);
+        const uint32_t gnum = (uint32_t)(v.acc2 >> 32) + (uint32_t)(2 * (2 * cnt - (E - 1)));
+        const uint32_t sum_topo = (uint32_t)v.acc2 + (uint32_t)tl;
+        v.acc2 = ((uint64_t)gnum << 32) | sum_topo;
+        v.acc3 += (uint64_t)node_cost(em_type(emA));
+        v.s.acc = v.s.acc < 0xFFFF ? v.s.acc + 1 : 0xFFFF;
+        if (v.s.rz == zA) v.s.intra = v.s.intra < 0xFFFF ? v.s.intra + 1 : 0xFFFF;
+        v.sum_lat += sel_lat;
+        v.sum_cpu += sel_cpu;
+        // increase_resources / increase_endpoint_latency (:674-677) and the same step's
+        // decrease in next_request() (:1137-1143) -> the history counters advance
+        const uint32_t edA_new = ((oA == ai ? (uint32_t)Mn : (uint32_t)ed_M(edA)) << 20) |
+                                 ((uint32_t)Mn << 10) | (uint32_t)jn;
+        if constexpr (ED_REGS) {
+            // select-stores over constant indices (a runtime-indexed store would move ed[]
+            // out of registers)
+#pragma unroll
+            for (int e = 0; e < TPE_E; ++e) {
+                const uint32_t edo = e == oA ? (ed[e] & ~(0x3FFu << 20)) | ((uint32_t)Mn << 20) : ed[e];
+                ed[e] = e == ai ? edA_new : edo;
+            }
+        } else if (keep) {
+            if (oA != ai) *(p.edyn + (int64_t)oA * p.B + env) = ((edO & ~(0x3FFu << 20)) | ((uint32_t)Mn << 20));
+            *(p.edyn + (int64_t)ai * p.B + env) = (edA_new);
+        }
+        v.s.penalty = 0;
+        reward = accept_reward(p, sel_lat, tl, sel_cpu, v.acc2, v.s.acc);
+        v.last_r = reward;
+    } else if (reject) {
+        v.s.penalty = 1;
+        reward = p.reward_fn == LB_REWARD_LATENCY ? -1000.0 : -1.0;
+        v.last_r = reward;
+    } else {  // unrecognised action (:685-686): penalty and selected_* stay stale
+        reward = p.reward_fn == LB_REWARD_NAIVE ? (v.s.penalty ? -1.0 : 1.0) : v.last_r;
+    }
+    v.total += reward;
+
+    // ---- next_request (:1131-1163)
+    {
+        double x1, x2;
+        int r, n;
+        tpe_request_draws<TRACE>(p, ev, (uint32_t)(v.acc3 >> 32), (uint32_t)v.s.step, false, x1, x2, r, n);
+        const double arrival = v.t + x1;
+        const double departure = arrival + x2;
+        v.dt = departure - arrival;
+        v.t = arrival;
+        v.s.thr_idx = (r + 6) % 7;  // endpoint_list[r - 1] (:1117)
+        if constexpr (stored) {
+            const uint64_t word = n < 32 ? v.nz0 : (n < 64 ? v.nz1 : p.nzone[(int64_t)(n >> 5) * p.B + ev]);
+            v.s.rz = (int)((word >> (2 * (n & 31))) & 3);
+        } else {  // the zone of the request's node (:1120-1121), drawn again
+            int ty, zo, cpu;
+            node_draw<false>(p, ev, (uint32_t)(v.acc3 >> 32), n, ty, zo, cpu);
+            v.s.rz = zo;
+        }
+    }
+    return reward;
+}
+
+
 // step() (:403-513) fused with next_request(), get_state(), reward and done.  RECOMPUTE
 // (Philox mode, many envs): the scenario is redrawn instead of loaded.
 // VecEnv auto-reset: an env whose episode ends gets its terminal obs and episode-stats row,
@@ -342,104 +480,9 @@ __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
     const bool done = live && v.s.step == p.L;  // (:472)
     const bool do_reset = done && p.auto_reset;
     const bool keep = live && !do_reset;  // the state stores reset() below does not redo
-    const bool accept = a >= -E && a < E;
-    const bool reject = a == E;
-    if (a < -E) v.s.bad = 1;  // reference: IndexError; here: treated as unrecognised
-    if (!v.s.reset_done) v.s.bad = 1;
-    const int ai = accept ? (a < 0 ? a + E : a) : 0;
-    uint32_t emA = em[0], edA = ed[0];
-    double lat0A = lat0[0];
-#pragma unroll
-    for (int e = 1; e < TPE_E; ++e)
-        if (ai == e) { emA = em[e]; edA = ed[e]; lat0A = lat0[e]; }
-    const int oA = em_owner(emA);
-    uint32_t edO = ed[0];
-#pragma unroll
-    for (int e = 1; e < TPE_E; ++e)
-        if (oA == e) edO = ed[e];
-    const int jA = ed_j(edA);
-    const int Mn = ed_M(edO) < CMAX ? ed_M(edO) + 1 : CMAX;
-    const int jn = jA < CMAX ? jA + 1 : CMAX;
-    const int k0A = (int)lat0A, c0A = em_c0(emA);
-    const double lut_selA = p.lat_lut[(jA) * LAT_ROWS + k0A];
-    const double sel_cpu = p.cpu_lut[(ed_m(edA)) * CPU_ROWS + c0A];
-    const double next_lat = p.lat_lut[(jn) * LAT_ROWS + k0A];
-    const double next_cpu = p.cpu_lut[(Mn) * CPU_ROWS + c0A];
-    int cnt = 0;  // #{e != ai : loads[e] <= loads[ai]} for the O(E) Gini update
-#pragma unroll
-    for (int e = 0; e < TPE_E; ++e) {
-        if (e < E) {
-            const int j = ed_j(ed[e]);
-            // table rows 0 are the initial values: only endpoints selected (j > 0) /
-            // refreshed (m > 0) this episode gather from the LUTs
-            const int m = ed_m(ed[e]);
-            double l = lat0[e], c = (double)em_c0(em[e]);
-            if (j) l = p.lat_lut[j * LAT_ROWS + (int)lat0[e]];
-            if (m) c = p.cpu_lut[m * CPU_ROWS + em_c0(em[e])];
-            float ol = (float)l;
-            float oc = (float)c;
-            if (accept && e == ai) { ol = (float)next_lat; oc = (float)next_cpu; }
-            const int z = em_zone(em[e]);
-            me[4 + 3 * e] = (uint32_t)z | ((uint32_t)zcap_val(v.zcap, z) << 2);
-            me[5 + 3 * e] = __float_as_uint(oc);
-            me[6 + 3 * e] = __float_as_uint(ol);
-            if (e != ai && j <= jA) ++cnt;
-        }
-    }
-
-    // ---- take_action (:578-686)
-    double reward;
-    if (accept) {
-        const int zA = em_zone(emA);
-        const double sel_lat = jA == 0 ? lat0A : lut_selA;
-        const int tl = topo_val(v.topo, v.s.rz, zA);
-        const uint32_t gnum = (uint32_t)(v.acc2 >> 32) + (uint32_t)(2 * (2 * cnt - (E - 1)));
-        const uint32_t sum_topo = (uint32_t)v.acc2 + (uint32_t)tl;
-        v.acc2 = ((uint64_t)gnum << 32) | sum_topo;
-        v.acc3 += (uint64_t)node_cost(em_type(emA));
-        v.s.acc = v.s.acc < 0xFFFF ? v.s.acc + 1 : 0xFFFF;
-        if (v.s.rz == zA) v.s.intra = v.s.intra < 0xFFFF ? v.s.intra + 1 : 0xFFFF;
-        v.sum_lat += sel_lat;
-        v.sum_cpu += sel_cpu;
-        // increase_resources / increase_endpoint_latency (:674-677) and the same step's
-        // decrease in next_request() (:1137-1143) -> the history counters advance
-        const uint32_t edA_new = ((oA == ai ? (uint32_t)Mn : (uint32_t)ed_M(edA)) << 20) |
-                                 ((uint32_t)Mn << 10) | (uint32_t)jn;
-        if (keep) {
-            if (oA != ai) *(p.edyn + (int64_t)oA * p.B + env) = ((edO & ~(0x3FFu << 20)) | ((uint32_t)Mn << 20));
-            *(p.edyn + (int64_t)ai * p.B + env) = (edA_new);
-        }
-        v.s.penalty = 0;
-        reward = accept_reward(p, sel_lat, tl, sel_cpu, v.acc2, v.s.acc);
-        v.last_r = reward;
-    } else if (reject) {
-        v.s.penalty = 1;
-        reward = p.reward_fn == LB_REWARD_LATENCY ? -1000.0 : -1.0;
-        v.last_r = reward;
-    } else {  // unrecognised action (:685-686): penalty and selected_* stay stale
-        reward = p.reward_fn == LB_REWARD_NAIVE ? (v.s.penalty ? -1.0 : 1.0) : v.last_r;
-    }
-    v.total += reward;
-
-    // ---- next_request (:1131-1163)
-    {
-        double x1, x2;
-        int r, n;
-        tpe_request_draws<TRACE>(p, ev, (uint32_t)(v.acc3 >> 32), (uint32_t)v.s.step, false, x1, x2, r, n);
-        const double arrival = v.t + x1;
-        const double departure = arrival + x2;
-        v.dt = departure - arrival;
-        v.t = arrival;
-        v.s.thr_idx = (r + 6) % 7;  // endpoint_list[r - 1] (:1117)
-        if constexpr (stored) {
-            const uint64_t word = n < 32 ? v.nz0 : (n < 64 ? v.nz1 : p.nzone[(int64_t)(n >> 5) * p.B + ev]);
-            v.s.rz = (int)((word >> (2 * (n & 31))) & 3);
-        } else {  // the zone of the request's node (:1120-1121), drawn again
-            int ty, zo, cpu;
-            node_draw<false>(p, ev, (uint32_t)(v.acc3 >> 32), n, ty, zo, cpu);
-            v.s.rz = zo;
-        }
-    }
+    float no_olat[TPE_E], no_ocpu[TPE_E];  // (unused: the single step gathers the observed values)
+    const double reward = tpe_step_core<TRACE, stored, false>(p, ev, env, keep, v, lat0, em, ed, no_olat, no_ocpu,
+                                                              a, me);
     if (live) {
         if (p.reward) *(p.reward + env) = ((float)reward);
         if (p.done) p.done[env] = (uint8_t)done;
@@ -494,4 +537,410 @@ __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
     }
 }
 
+// envs/baselines.py (:6-35) on one lane's registers (k_policy's values): argmin topology
+// latency / argmax zone cpu capacity / argmin endpoint cpu over feasible = mask[:-1]
+// (masks are all True, :808-821), first index on ties; or the uniform random action.
+// (The kind is a template parameter: the endpoint-cpu gathers would otherwise hold
+// registers in every instantiation of the rollout.)
+template <int KIND>
+__device__ __forceinline__ int tpe_policy(const Params& p, int64_t ev, const TEnv& v, const uint32_t (&em)[TPE_E],
+                                          const uint32_t (&ed)[TPE_E]) {
+    if constexpr (KIND == LB_POLICY_RANDOM) return random_action(p, ev, v.acc3, v.s.step);
+    const int nf = p.A - 1;
+    if (nf <= 0) return p.A - 1;
+    double best = 0.0;
+    int bi = 0;
+#pragma unroll
+    for (int e = 0; e < TPE_E; ++e) {
+        if (e >= nf) continue;
+        const int z = em_zone(em[e]);
+        double val;
+        if constexpr (KIND == LB_POLICY_TOPOLOGY_GREEDY) val = (double)topo_val(v.topo, z, v.s.rz);
+        else if constexpr (KIND == LB_POLICY_ZONE_CPU_GREEDY) val = -(double)zcap_val(v.zcap, z);
+        else val = cpu_of(p, em[e], ed[e]);
+        if (e == 0 || val < best) { best = val; bi = e; }
+    }
+    return bi;
+}
+
+// lb_rollout on the thread-per-env layout: K vector steps under an on-device policy in ONE
+// launch, each lane's env held in registers from the first step to the last (including the
+// observed latency / cpu of every endpoint, so a step gathers 4 table values); step k's
+// obs / reward / done / action go to slot k.  The state is read once and written once per
+// launch instead of once per step, and there is one launch ramp per K steps.
+// Observations: each lane writes its env's finished (R x 8) float32 rows into the wave's LDS
+// image (a 76-word stride per lane: 16-byte writes of 8 consecutive lanes cover all 32
+// banks), and the wave copies its 64 envs' rows out as contiguous float4 runs; building
+// the rows once per env instead of decoding a compact image per stored piece took the
+// copy-out from about half of the step's VALU instructions to a load and a store.
+// Auto-reset: each wave lists its finishing envs in its image region (as k_step_tpe), and
+// after an LDS-only block barrier the block's waves run the listed resets RO_RW = 64 lanes
+// per env, one env per wave per round; a reset writes the env's post-reset obs into slot k and its
+// new episode (scenario, clock, request) into an LDS record, from which the owning lane
+// reloads its registers after a second barrier.  Nothing but the outputs leaves the CU
+// between steps, so no barrier waits on global stores.  Needs N <= 64 (the node-zone words
+// stay in registers).  Bit for bit K x (lb_policy + lb_step) (tests/test_gpu_api.py).
+constexpr int RS_REC_W = 40;   // LDS record of a reset: lat0 (16), emeta (8), topo, zcap, nz0, nz1, t, acc3, sc
+constexpr int RO_STRIDE = 19;  // float4 per lane in the rollout's obs image (2R <= 18, + 1 pad)
+constexpr int RO_REC_OFF = 512;  // words: a wave region's reset records, past its list (<= 449 words)
+// lanes per reset in the rollout: a whole wave per finishing env (the 24 node draws, 8
+// endpoint draws and the request in parallel, a chain about 3 Philox blocks deep), each of
+// the block's waves takes one listed env per round.  With staggered episodes a 256-env
+// block has ~2.6 finishing envs per step: 8-lane groups left three waves parked at the
+// barrier behind one wave's 5-block-deep reset chain (2^20 envs: 111 us per step vs 78
+// lockstep).
+constexpr int RO_RW = 64;
+
+// get_state() (:688-758) rows of this lane's env from registers, into its LDS image
+__device__ __forceinline__ void tpe_obs_rows(const Params& p, float4* row, const TEnv& v,
+                                             const uint32_t (&em)[TPE_E], const float (&olat)[TPE_E],
+                                             const float (&ocpu)[TPE_E]) {
+    const float rz = (float)v.s.rz, thr = (float)threshold(v.s.thr_idx), dt = (float)v.dt;
+#pragma unroll
+    for (int e = 0; e < TPE_E; ++e) {
+        if (e < p.E) {
+            const int z = em_zone(em[e]);
+            row[2 * e] = make_float4((float)z, (float)zcap_val(v.zcap, z), ocpu[e], (float)topo_val(v.topo, z, v.s.rz));
+            row[2 * e + 1] = make_float4(olat[e], rz, thr, dt);
+        }
+    }
+    if (p.R > p.E) {  // the reject row
+        row[2 * p.E] = make_float4(-1.f, -1.f, -1.f, -1.f);
+        row[2 * p.E + 1] = make_float4(-1.f, rz, thr, dt);
+    }
+}
+
+// the wave's envs' rows from its image as contiguous float4 runs (G envs per store
+// instruction); m = the wave's finishing envs, which = COPY_ALL / FLAGGED / UNFLAGGED
+__device__ __forceinline__ void tpe_copy_rows(const Params& p, float* out, const float4* wimg, int64_t env0,
+                                              uint64_t m, int which) {
+    const int lane = threadIdx.x & 63;
+    const int P = 2 * p.R;
+    const int G = 64 / P;
+    const int eo = lane / P, piece = lane - eo * P;
+    if (eo >= G) return;
+    const int64_t left = p.B - env0;
+    const int nenv = left < 64 ? (int)left : 64;
+    float4* base = reinterpret_cast<float4*>(out + env0 * (int64_t)p.R * 8) + piece;
+    for (int el = eo; el < nenv; el += G) {
+        if (which != COPY_ALL && (which == COPY_FLAGGED) != (((m >> el) & 1) != 0)) continue;
+        st_stream(base + el * P, wimg[el * RO_STRIDE + piece]);
+    }
+}
+
+// The next episode of an env, as reset() (:290-400) draws it in Philox mode, into its
+// RO_REC_BYTES record (p.rec): W lanes per env, lane e < E its endpoint (the same draws and
+// owner rule as slice_reset).  Words: lat0 [0,16), emeta [16,24), topo, zcap, nz0, nz1, the
+// first request's x1, x2 (f64) [24,36), thr_idx | rz << 8 [36].  The clock is not in it:
+// arrival = t + x1 is applied when the episode starts.
+template <int W>
+__device__ __forceinline__ void tpe_write_record(const Params& p, int64_t env, uint32_t episode, int lane) {
+    uint64_t zc = 0, nz0 = 0, nz1 = 0;
+    for (int w = 0; w < p.NZW; ++w) {  // nodes (:349-373)
+        uint64_t word = 0;
+        for (int n = 32 * w + lane; n < 32 * (w + 1) && n < p.N; n += W) {
+            int ty, zo, cpu;
+            node_draw<false>(p, env, episode, n, ty, zo, cpu);
+            zc += (uint64_t)node_cpu_int(ty) << (16 * zo);
+            word |= (uint64_t)zo << (2 * (n & 31));
+        }
+        word = slice_or64<W>(word);
+        if (w == 0) nz0 = word;
+        if (w == 1) nz1 = word;
+    }
+    zc = slice_sum64<W>(zc);
+    double lat0 = 0.0;  // endpoints (:328, :379-386)
+    int node = 0;
+    if (lane < p.E) {
+        const U4 d = draw(p, env, episode, (uint32_t)lane, D_EP);
+        lat0 = 1.0 + 99.0 * u53(d.x, d.y);
+        node = (int)bounded(d.z, 24);
+    }
+    int owner = lane;  // first endpoint hosted on the same node
+    for (int e2 = 0; e2 < p.E; ++e2) {
+        const int nd2 = (int)shfl_u32<W>((uint32_t)node, e2);
+        if (nd2 == node && e2 < owner) owner = e2;
+    }
+    uint32_t* out = reinterpret_cast<uint32_t*>(p.rec + env * (RO_REC_BYTES / 16));
+    if (lane < p.E) {
+        int ty, zo, cpu;
+        node_draw<false>(p, env, episode, node, ty, zo, cpu);
+        const uint64_t lb = (uint64_t)__double_as_longlong(lat0);
+        *reinterpret_cast<uint2*>(out + 2 * lane) = make_uint2((uint32_t)lb, (uint32_t)(lb >> 32));
+        out[16 + lane] = em_pack(zo, owner, ty, cpu, node);
+    }
+    const uint64_t topo = scen_topo(p, env, episode);  // (:331-338)
+    double x1, x2;  // next_request() closing reset() (:397)
+    int r, n;
+    slice_request_draws<W, false>(p, env, episode, 0, lane, true, x1, x2, r, n);
+    if (lane == 0) {
+        const int rz = (int)(((n < 32 ? nz0 : nz1) >> (2 * (n & 31))) & 3);
+        const uint64_t w[6] = {topo, zc, nz0, nz1, (uint64_t)__double_as_longlong(x1),
+                               (uint64_t)__double_as_longlong(x2)};
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+            *reinterpret_cast<uint2*>(out + 24 + 2 * j) = make_uint2((uint32_t)w[j], (uint32_t)(w[j] >> 32));
+        out[36] = (uint32_t)((r + 6) % 7) | ((uint32_t)rz << 8);
+    }
+}
+
+// reset() from the env's record: the episode counter advances, the clock runs on (t is
+// never reset, :1135), the first request arrives at t + x1
+// (q: the record's first 38 words, loaded at the start of the step so the load overlaps it)
+__device__ __forceinline__ void tpe_start_episode(const Params& p, const uint4 (&q)[10], TEnv& v,
+                                                  double (&lat0)[TPE_E], uint32_t (&em)[TPE_E],
+                                                  uint32_t (&ed)[TPE_E], float (&olat)[TPE_E],
+                                                  float (&ocpu)[TPE_E]) {
+    uint32_t w[40];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+        w[4 * j] = q[j].x; w[4 * j + 1] = q[j].y; w[4 * j + 2] = q[j].z; w[4 * j + 3] = q[j].w;
+    }
+    auto u64 = [&](int i) { return (uint64_t)w[i] | ((uint64_t)w[i + 1] << 32); };
+#pragma unroll
+    for (int e = 0; e < TPE_E; ++e) {
+        lat0[e] = e < p.E ? __longlong_as_double((long long)u64(2 * e)) : 0.0;
+        em[e] = e < p.E ? w[16 + e] : 0u;
+        ed[e] = 0u;
+        olat[e] = (float)lat0[e];  // table rows 0: the initial values
+        ocpu[e] = (float)em_c0(em[e]);
+    }
+    v.topo = u64(24);
+    v.zcap = u64(26);
+    v.nz0 = u64(28);
+    v.nz1 = u64(30);
+    const uint32_t episode = (uint32_t)(v.acc3 >> 32) + 1;
+    v.acc3 = (uint64_t)episode << 32;
+    v.acc2 = 0;
+    v.sum_lat = 0.0;
+    v.sum_cpu = 0.0;
+    v.total = 0.0;
+    v.last_r = p.init_last_r;
+    v.s.step = 0; v.s.acc = 0; v.s.intra = 0; v.s.penalty = 0; v.s.reset_done = 1;
+    v.s.thr_idx = (int)(w[36] & 7);
+    v.s.rz = (int)((w[36] >> 8) & 3);
+    const double arrival = v.t + __longlong_as_double((long long)u64(32));
+    const double departure = arrival + __longlong_as_double((long long)u64(34));
+    v.dt = departure - arrival;
+    v.t = arrival;
+}
+
+template <int NB, int KIND, bool PRE>
+__global__ __launch_bounds__(NB) void k_rollout_tpe(Params p, int K, int32_t* act_out) {
+    constexpr int NW = NB / 64, RS_ROUND = NW * (64 / RO_RW);
+    __shared__ float4 oimg[NW][64 * RO_STRIDE];
+    __shared__ uint32_t cnt[2][NW];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float4* wimg = oimg[wv];
+    uint32_t* wreg = reinterpret_cast<uint32_t*>(wimg);  // the region as words (list, records)
+    float4* mine = wimg + lane * RO_STRIDE;
+    const int64_t env0 = (int64_t)blockIdx.x * NB + (threadIdx.x & ~63);
+    const int64_t env = env0 + lane;
+    const bool live = env < p.B;
+    const int64_t ev = live ? env : 0;  // dead lanes step env 0's copy in registers and store nothing
+    const int E = p.E;
+
+    TEnv v;
+    double lat0[TPE_E];
+    uint32_t em[TPE_E], ed[TPE_E];
+#pragma unroll
+    for (int e = 0; e < TPE_E; ++e) {
+        const int64_t i = (int64_t)e * p.B + ev;
+        lat0[e] = e < E ? p.lat0[i] : 0.0;
+        em[e] = e < E ? p.emeta[i] : 0u;
+        ed[e] = e < E ? p.edyn[i] : 0u;
+    }
+    v.t = p.t[ev];
+    v.s = sc_unpack(p.sc[ev]);
+    v.zcap = p.zcap[ev];
+    v.acc2 = p.acc2[ev];
+    v.acc3 = p.acc3[ev];
+    v.topo = p.topo[ev];
+    v.nz0 = p.nzone[ev];
+    v.nz1 = p.NZW > 1 ? p.nzone[p.B + ev] : 0;
+    v.sum_lat = p.sum_lat[ev];
+    v.sum_cpu = p.sum_cpu[ev];
+    v.total = p.total[ev];
+    v.last_r = p.reward_fn != LB_REWARD_NAIVE ? p.last_r[ev] : 0.0;
+    float olat[TPE_E], ocpu[TPE_E];  // observed endpoint latency / cpu (obs columns 4, 2)
+#pragma unroll
+    for (int e = 0; e < TPE_E; ++e) {
+        olat[e] = e < E ? (float)lat_of(p, lat0[e], ed[e]) : 0.f;
+        ocpu[e] = e < E ? (float)cpu_of(p, em[e], ed[e]) : 0.f;
+    }
+    bool new_episode = false;  // the scenario arrays need writing back
+    const int64_t obs_slot = p.B * (int64_t)p.R * 8;
+    // episodes longer than the launch end at most once per env in it: their next episode is
+    // drawn here, before the first step, into the env's record (RS_W lanes per env, every
+    // finishing env of the wave in rounds of 8), and the step that ends one only reloads
+    // the registers from it -- no barrier and no serial reset chain inside the step loop.
+    // Shorter episodes take the in-loop block-list path below.
+    constexpr bool pre = PRE;  // (host: auto_reset && L > K)
+    if (pre) {
+        const int to_done = p.L - v.s.step;
+        const bool fin = live && to_done >= 1 && to_done <= K;
+        const uint64_t fm = __ballot(fin);
+        if (fin) {
+            uint32_t* it = wreg + 2 * __popcll(fm & ((1ull << lane) - 1));
+            it[0] = (uint32_t)lane;
+            it[1] = (uint32_t)(v.acc3 >> 32) + 1;
+        }
+        wave_lds_sync();
+        const int nf = __popcll(fm), g = lane / RS_W, gl = lane % RS_W;
+        for (int r0 = 0; r0 < nf; r0 += 64 / RS_W) {
+            const int i = r0 + g;
+            if (i < nf) tpe_write_record<RS_W>(p, env0 + (int64_t)wreg[2 * i], wreg[2 * i + 1], gl);
+        }
+        // the records are read back by other lanes of this wave; the list region becomes the
+        // first step's obs image
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+
+    for (int k = 0; k < K; ++k) {
+        uint4 q[10];  // the next episode's record, for an env this step ends
+        if (pre && live && v.s.step + 1 == p.L) {
+            const uint4* rp = p.rec + env * (RO_REC_BYTES / 16);
+#pragma unroll
+            for (int j = 0; j < 10; ++j) q[j] = rp[j];
+        }
+        const int a = tpe_policy<KIND>(p, ev, v, em, ed);
+        if (act_out && live) act_out[k * p.B + env] = a;
+        v.s.step = v.s.step < 0xFFFF ? v.s.step + 1 : 0xFFFF;
+        const bool done = live && v.s.step == p.L;  // (:472)
+        const bool do_reset = done && p.auto_reset;
+        const double reward =
+            tpe_step_core<false, true, true>(p, ev, env, false, v, lat0, em, ed, olat, ocpu, a, nullptr);
+        if (live) {
+            if (p.reward) p.reward[k * p.B + env] = (float)reward;
+            if (p.done) p.done[k * p.B + env] = (uint8_t)done;
+        }
+        const uint64_t m = __ballot(do_reset);
+        if (do_reset && p.ep_stats)
+            write_stats_row(p, p.ep_stats + env * LB_ST_K, v.s, v.acc2, v.acc3, v.total, v.sum_lat, v.sum_cpu);
+        float* obs_k = p.obs ? p.obs + k * obs_slot : nullptr;
+        if constexpr (PRE) {
+            if (p.term_obs && m) {  // the finishing envs' terminal rows first
+                if (do_reset) tpe_obs_rows(p, mine, v, em, olat, ocpu);
+                wave_lds_sync();
+                tpe_copy_rows(p, p.term_obs, wimg, env0, m, COPY_FLAGGED);
+                wave_lds_sync();
+            }
+            if (do_reset) {
+                tpe_start_episode(p, q, v, lat0, em, ed, olat, ocpu);
+                new_episode = true;
+            }
+            tpe_obs_rows(p, mine, v, em, olat, ocpu);
+            wave_lds_sync();
+            if (obs_k) tpe_copy_rows(p, obs_k, wimg, env0, m, COPY_ALL);
+            continue;
+        }
+        tpe_obs_rows(p, mine, v, em, olat, ocpu);
+        wave_lds_sync();
+        if (p.term_obs && m) tpe_copy_rows(p, p.term_obs, wimg, env0, m, COPY_FLAGGED);
+        if (obs_k) tpe_copy_rows(p, obs_k, wimg, env0, m, p.auto_reset ? COPY_UNFLAGGED : COPY_ALL);
+        if (!p.auto_reset) continue;  // uniform over the grid
+        wave_lds_sync();
+        if (do_reset) {  // the wave's list replaces its (copied-out) image
+            uint32_t* it = wreg + 1 + RS_LIST_W * __popcll(m & ((1ull << lane) - 1));
+            const uint64_t tb = (uint64_t)__double_as_longlong(v.t), sc = sc_pack(v.s);
+            it[0] = (uint32_t)env;
+            it[1] = (uint32_t)tb; it[2] = (uint32_t)(tb >> 32);
+            it[3] = (uint32_t)v.acc3; it[4] = (uint32_t)(v.acc3 >> 32);
+            it[5] = (uint32_t)sc; it[6] = (uint32_t)(sc >> 32);
+        }
+        // per-wave counts, double-buffered by step parity: a wave can be one barrier ahead
+        if (lane == 0) cnt[k & 1][wv] = (uint32_t)__popcll(m);
+        if (NW > 1) block_lds_sync();
+        else wave_lds_sync();
+        int pre[NW + 1];
+        pre[0] = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) pre[w + 1] = pre[w] + (int)cnt[k & 1][w];
+        const int mine_i = do_reset ? pre[wv] + __popcll(m & ((1ull << lane) - 1)) : -1;
+        const int g = lane / RO_RW, gl = lane % RO_RW;
+        for (int r0 = 0; r0 < pre[NW]; r0 += RS_ROUND) {  // uniform over the block
+            const int i = r0 + wv * (64 / RO_RW) + g;
+            if (i < pre[NW]) {
+                int q = 0;
+#pragma unroll
+                for (int w = 1; w < NW; ++w) q += i >= pre[w];
+                int base = 0;
+#pragma unroll
+                for (int w = 1; w < NW; ++w) base = q == w ? pre[w] : base;
+                const uint32_t* it = reinterpret_cast<const uint32_t*>(oimg[q]) + 1 + RS_LIST_W * (i - base);
+                const int64_t renv = (int64_t)it[0];
+                SEnv<1> sv;
+                sv.t = __longlong_as_double((long long)((uint64_t)it[1] | ((uint64_t)it[2] << 32)));
+                sv.acc3 = (uint64_t)it[3] | ((uint64_t)it[4] << 32);
+                sv.s = sc_unpack((uint64_t)it[5] | ((uint64_t)it[6] << 32));
+                slice_reset<RO_RW, 1, false, false>(p, renv, gl, sv);
+                if (obs_k) slice_write_obs<RO_RW, 1>(p, obs_k, renv, gl, sv);
+                // record (i - r0) lives in wave (i - r0) / 8's region, past its list: this group's
+                uint32_t* rc = wreg + RO_REC_OFF + g * RS_REC_W;
+                if (gl < E) {
+                    const uint64_t lb = (uint64_t)__double_as_longlong(sv.lat0[0]);
+                    rc[2 * gl] = (uint32_t)lb;
+                    rc[2 * gl + 1] = (uint32_t)(lb >> 32);
+                    rc[16 + gl] = sv.em[0];
+                }
+                if (gl == 0) {
+                    const uint64_t tb = (uint64_t)__double_as_longlong(sv.t), sc = sc_pack(sv.s);
+                    const uint64_t w8[7] = {sv.topo, sv.zcap, sv.nz0, sv.nz1, tb, sv.acc3, sc};
+#pragma unroll
+                    for (int j = 0; j < 7; ++j) {
+                        rc[24 + 2 * j] = (uint32_t)w8[j];
+                        rc[25 + 2 * j] = (uint32_t)(w8[j] >> 32);
+                    }
+                }
+            }
+            block_lds_sync();
+            if (mine_i >= r0 && mine_i < r0 + RS_ROUND) {  // the owner reloads its new episode
+                const int j = mine_i - r0;
+                const uint32_t* rc =
+                    reinterpret_cast<const uint32_t*>(oimg[j / (64 / RO_RW)]) + RO_REC_OFF + (j % (64 / RO_RW)) * RS_REC_W;
+                auto u64 = [&](int w) { return (uint64_t)rc[w] | ((uint64_t)rc[w + 1] << 32); };
+#pragma unroll
+                for (int e = 0; e < TPE_E; ++e) {
+                    lat0[e] = e < E ? __longlong_as_double((long long)u64(2 * e)) : 0.0;
+                    em[e] = e < E ? rc[16 + e] : 0u;
+                    ed[e] = 0u;
+                    olat[e] = (float)lat0[e];  // table rows 0: the initial values
+                    ocpu[e] = (float)em_c0(em[e]);
+                }
+                v.topo = u64(24);
+                v.zcap = u64(26);
+                v.nz0 = u64(28);
+                v.nz1 = u64(30);
+                v.t = __longlong_as_double((long long)u64(32));
+                v.acc3 = u64(34);
+                v.s = sc_unpack(u64(36));
+                v.acc2 = 0;
+                v.sum_lat = 0.0;
+                v.sum_cpu = 0.0;
+                v.total = 0.0;
+                v.last_r = p.init_last_r;
+                new_episode = true;
+            }
+            block_lds_sync();  // the records and lists are free for the next round / step
+        }
+    }
+    if (!live) return;
+#pragma unroll
+    for (int e = 0; e < TPE_E; ++e) {
+        if (e >= E) continue;
+        const int64_t i = (int64_t)e * p.B + env;
+        p.edyn[i] = ed[e];
+        if (new_episode) {
+            p.lat0[i] = lat0[e];
+            p.emeta[i] = em[e];
+        }
+    }
+    if (new_episode) {
+        p.topo[env] = v.topo;
+        p.zcap[env] = v.zcap;
+        p.nzone[env] = v.nz0;
+        if (p.NZW > 1) p.nzone[p.B + env] = v.nz1;
+    }
+    tpe_store_scalars(p, env, v);
+}
 }  // namespace lbk

@@ -163,10 +163,12 @@ int lb_step(void* state, const lb_config* cfg, int64_t num_envs, const int32_t* 
  * the run_baselines.py loop (:60-78) and BASELINE config 2's random policy without a launch
  * per vector step.  Step k writes obs_out + k*B*R*8, reward_out + k*B, done_out + k*B and
  * actions_out + k*B (each NULL = skip); with cfg.auto_reset, terminal_obs_out / ep_stats_out
- * as in lb_step (an env finishing twice keeps its last).  Philox mode only.  The slice state
- * layout runs all K steps in one launch with the state in registers; the thread-per-env
- * layout (E <= 8, many envs) issues K policy + step launches and needs actions_out for the
- * greedy policies. */
+ * as in lb_step (an env finishing twice keeps its last).  Philox mode only.  Both state
+ * layouts run all K steps in one launch with the state in registers (k_rollout_slice,
+ * k_rollout_tpe; the latter draws the next episode of every env that ends inside the launch
+ * before its first step, into a scratch record that is part of the state layout); the
+ * thread-per-env layout with num_nodes > 64 issues K policy + step launches instead and
+ * then needs actions_out for the greedy policies. */
 int lb_rollout(void* state, const lb_config* cfg, int64_t num_envs, int32_t policy, int32_t steps,
                float* obs_out, float* reward_out, uint8_t* done_out, int32_t* actions_out,
                float* terminal_obs_out, double* ep_stats_out, void* stream);

@@ -270,7 +270,9 @@ def test_vecmonitor_file_during_training(tmp_path):
     (3000, dict(num_endpoints=64, reward_function="multi"), "auto"),
     (40000, dict(num_endpoints=20, reward_function="fairness"), "auto"),       # 4-envs-per-wave slice
     (40000, {}, "slice"),
-    (40000, dict(num_endpoints=6), "tpe"),                                     # K policy + step launches
+    (40000, dict(num_endpoints=6), "tpe"),                                     # k_rollout_tpe, 64-thread blocks
+    (70000, {}, "tpe"),                                                        # k_rollout_tpe, 256-thread blocks
+    (40000, dict(num_nodes=100), "tpe"),                                       # N > 64: K policy + step launches
 ])
 @pytest.mark.parametrize("kind", ["random", "topo", "zone_cpu", "endpoint_cpu"])
 def test_rollout_equals_policy_plus_step(B, kw, geometry, kind):
@@ -302,6 +304,49 @@ def test_rollout_equals_policy_plus_step(B, kw, geometry, kind):
     # the env goes on from where the rollout left it
     a_env.step_device(act[0])
     b_env.step_device(act[0])
+    assert torch.equal(a_env.obs, b_env.obs)
+    assert a_env.status() == 0
+
+
+@pytest.mark.parametrize("B,kw", [(40000, dict(num_endpoints=6, reward_function="multi")), (70000, {}),
+                                  (131072, dict(reward_function="latency"))])
+@pytest.mark.parametrize("kind", ["random", "endpoint_cpu"])
+@pytest.mark.parametrize("K,L", [(23, 9), (16, 20)])
+def test_rollout_tpe_staggered_equals_policy_plus_step(B, kw, kind, K, L):
+    """k_rollout_tpe with staggered episodes (1/L of the envs finish at every step, the
+    bench's steady state): == K x (lb_policy + lb_step), bit for bit, including the terminal
+    obs and the episode-stats rows.  L <= K: envs can finish twice in a launch (in-loop
+    block-list resets); L > K: next episodes drawn into records before the first step."""
+    from lbk8s import LBVecEnv
+    envs = [LBVecEnv(B, seed=5, as_tensors=True, episode_length=L, geometry="tpe", **kw) for _ in range(2)]
+    gid = torch.arange(B, device="cuda")
+    for e in envs:
+        e.reset()
+        for r in range(1, L):
+            e.step_device(None)
+            e.reset_masked((gid % L) == r)
+    a_env, b_env = envs
+    R = a_env.cfg.obs_rows
+    obs = torch.empty((K, B, R, 8), device="cuda")
+    rew = torch.empty((K, B), device="cuda")
+    dn = torch.empty((K, B), dtype=torch.uint8, device="cuda")
+    act = torch.empty((K, B), dtype=torch.int32, device="cuda")
+    a_env.rollout(kind, K, obs_out=obs, reward_out=rew, done_out=dn, actions_out=act)
+    for k in range(K):
+        ak = b_env.policy(kind)
+        assert torch.equal(act[k], ak), k
+        b_env.step_device(ak)
+        assert torch.equal(obs[k], b_env.obs), k
+        assert torch.equal(rew[k], b_env.rewards), k
+        assert torch.equal(dn[k], b_env.dones), k
+        assert 0 < int(dn[k].sum()) < B
+    assert torch.equal(a_env.stats(), b_env.stats())
+    assert torch.equal(a_env.terminal_obs, b_env.terminal_obs)
+    assert torch.equal(a_env.ep_stats, b_env.ep_stats)
+    for f in ("endpoint_latency", "endpoint_cpu_usage_percentage", "avg_load_served", "current_time"):
+        assert torch.equal(a_env.field(f), b_env.field(f)), f
+    a_env.step_device(None)
+    b_env.step_device(None)
     assert torch.equal(a_env.obs, b_env.obs)
     assert a_env.status() == 0
 

@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--config1", action="store_true")
     ap.add_argument("--rollout", action="store_true")
     ap.add_argument("--lib", default=None, help="another build of liblbk8s.so (A/B)")
+    ap.add_argument("--geometry", default="auto", help="--rollout: state layout (auto / tpe / slice)")
     args = ap.parse_args()
     if args.lib:
         from lbk8s import _native
@@ -159,7 +160,7 @@ def rollout(torch, LBVecEnv, dev, args):
             B = 1 << lg
             if name == "e64_multi" and lg > 20:
                 continue
-            env = LBVecEnv(B, device=dev, seed=0, as_tensors=True, geometry="slice", **CONFIGS[name])
+            env = LBVecEnv(B, device=dev, seed=0, as_tensors=True, geometry=args.geometry, **CONFIGS[name])
             R, T = env.cfg.obs_rows, args.ring
             ring = torch.empty((T, B, R, 8), dtype=torch.float32, device=dev)
             rew = torch.empty((T, B), dtype=torch.float32, device=dev)
@@ -180,7 +181,7 @@ def rollout(torch, LBVecEnv, dev, args):
             b_step = algorithmic_bytes(env.cfg, reads_actions=False)
             out_b = 32 * R + 5
             b = out_b + (b_step - out_b) / T
-            print(json.dumps(dict(config=name, envs=B, mode=f"lb_rollout_random_k{T}", ms_per_step=round(ms, 5),
+            print(json.dumps(dict(config=name, envs=B, mode=f"lb_rollout_random_k{T}", geometry=args.geometry, ms_per_step=round(ms, 5),
                                   env_steps_per_s=B / ms * 1e3, alg_GBps=b * B / ms / 1e6,
                                   bytes_per_env_step=round(b, 1))), flush=True)
             del env, ring, rew, dn

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Workload for the rocprofv3 PMC passes: bench.py's timed step (2^20 default envs, the
 env's random policy drawn in the kernel, obs / reward / done ring of 16, episodes staggered
-so 1/episode_length of the envs end and auto-reset every step), 16 launches after the
-stagger setup, then 3 torch copies of 1 GiB (known bytes: calibrates FETCH_SIZE /
+so 1/episode_length of the envs end and auto-reset every step), 16 lb_step launches after
+the stagger setup (PMC_MODE=rollout: 8 lb_rollout launches of 16 steps, bench.py's default
+launch shape), then 3 torch copies of 1 GiB (known bytes: calibrates FETCH_SIZE /
 WRITE_SIZE)."""
 import os
 import sys
@@ -34,8 +35,12 @@ def main():
         env.step_device(None, obs_out=ring[0], reward_out=rew[0], done_out=done[0])
         env.reset_masked((gid % L) == r)
     torch.cuda.synchronize()
-    for i in range(16):
-        env.step_device(None, obs_out=ring[i % T], reward_out=rew[i % T], done_out=done[i % T])
+    if os.environ.get("PMC_MODE") == "rollout":
+        for i in range(8):
+            env.rollout("random", T, obs_out=ring, reward_out=rew, done_out=done)
+    else:
+        for i in range(16):
+            env.step_device(None, obs_out=ring[i % T], reward_out=rew[i % T], done_out=done[i % T])
     torch.cuda.synchronize()
     x = torch.empty(1 << 28, dtype=torch.float32, device="cuda").uniform_()
     y = torch.empty_like(x)

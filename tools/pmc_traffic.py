@@ -32,16 +32,19 @@ def main():
     ap.add_argument("--config", default="default")
     ap.add_argument("--envs", type=int, default=1 << 20)
     ap.add_argument("--out", default="profiles/pmc_traffic.json")
+    ap.add_argument("--steps-per-launch", type=int, default=16, help="lb_rollout launches: vector steps each")
     args = ap.parse_args()
     f = per_kernel(args.fetch_csv, "FETCH_SIZE")
     w = per_kernel(args.write_csv, "WRITE_SIZE")
-    step = [k for k in f if "k_step" in k][0]
+    roll = [k for k in f if "k_rollout" in k]
+    step = roll[0] if roll else [k for k in f if "k_step" in k][0]
+    steps_per_launch = args.steps_per_launch if roll else 1
     copy = [k for k in f if "copyBuffer" in k]
     copy_bytes = float(1 << 30)
     factor = copy_bytes / statistics.median(f[copy[0]]) if copy else 2.0
-    # the last 16 launches are the timed-step workload (earlier ones: the stagger setup)
-    fetch_raw = statistics.median(f[step][-13:])
-    write = statistics.median(w[step][-13:])
+    # the last launches are the timed-step workload (earlier ones: the stagger setup)
+    fetch_raw = statistics.median(f[step][-(6 if roll else 13):])
+    write = statistics.median(w[step][-(6 if roll else 13):])
     rs = [k for k in f if "k_reset_listed" in k]  # builds before the in-step auto-reset
     reset = None
     if rs:
@@ -51,10 +54,12 @@ def main():
                fetch_size_raw_bytes=fetch_raw, fetch_correction=factor,
                read_bytes=fetch_raw * factor, write_bytes=write,
                hbm_bytes_per_launch=fetch_raw * factor + write,
-               hbm_bytes_per_env_step=(fetch_raw * factor + write) / args.envs,
+               steps_per_launch=steps_per_launch,
+               hbm_bytes_per_env_step=(fetch_raw * factor + write) / args.envs / steps_per_launch,
                reset_kernel=reset,
                step_plus_reset_bytes_per_env_step=(fetch_raw * factor + write
-                                                   + (reset["hbm_bytes_per_launch"] if reset else 0.0)) / args.envs,
+                                                   + (reset["hbm_bytes_per_launch"] if reset else 0.0))
+               / args.envs / steps_per_launch,
                calibration="1 GiB device copy: write = %.3f GiB, raw fetch = %.3f GiB" % (
                    statistics.median(w[copy[0]]) / copy_bytes if copy else float("nan"),
                    statistics.median(f[copy[0]]) / copy_bytes if copy else float("nan")))
