@@ -317,7 +317,12 @@ def main(argv=None):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
                      "kernel_ms": kernel_ms, "bytes_per_env_step": b_alg, "envs_per_launch": B,
-                     "steps_per_launch": T if args.launch == "rollout" else 1},
+                     "steps_per_launch": T if args.launch == "rollout" else 1,
+                     # one launch = steps_per_launch vector steps: the rocprof average duration
+                     # of the kernel is launch_ms; traffic is HBM bytes per launch (PMC)
+                     "launch_ms": kernel_ms * (T if args.launch == "rollout" else 1),
+                     "traffic_bytes_per_env_step": (traffic / B / (T if args.launch == "rollout" else 1)
+                                                    if traffic is not None else None)},
     }
     if step_res is not None:
         ks = step_res["kernel_ms"]

@@ -1,11 +1,18 @@
-# bench.py at the per-GPU env counts of config 3 strong-scaled to 1/2/4/8 GPUs (one GPU)
+#!/bin/bash
+# bench.py at the strong-scaling shard sizes (1M envs over 1/2/4/8 GPUs), one GPU, both
+# launch shapes per run -> gpurun_out/strong_sizes.jsonl
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-TAG=${TAG:-r02}
-: > gpurun_out/sizes_${TAG}.jsonl
+: > gpurun_out/strong_sizes.jsonl
 for n in 131072 262144 524288 1048576; do
-  timeout -k 10 200 python bench.py --weak --envs $n --no-cpu-baseline > gpurun_out/sizes_${TAG}_$n.log 2>&1 || exit 1
-  grep -h '"metric"' gpurun_out/sizes_${TAG}_$n.log >> gpurun_out/sizes_${TAG}.jsonl
-  tail -1 gpurun_out/sizes_${TAG}_$n.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print($n, round(d['ms_per_step']*1000,2), 'us', '%.3g' % d['value'])"
+  timeout -k 10 200 python3 bench.py --weak --envs $n --no-cpu-baseline > gpurun_out/sizes_one.log 2>&1 || { cat gpurun_out/sizes_one.log; exit 1; }
+  tail -1 gpurun_out/sizes_one.log >> gpurun_out/strong_sizes.jsonl
 done
+python3 - <<'PY'
+import json
+for l in open("gpurun_out/strong_sizes.jsonl"):
+    d = json.loads(l)
+    print(d["config"]["envs_per_gpu"], "rollout %.2f us (%.3e/s, frac %.3f)" % (d["roofline"]["kernel_ms"] * 1e3, d["value"], d["roofline"]["frac"]),
+          "lb_step %.2f us (%.3e/s)" % (d["lb_step"]["kernel_ms"] * 1e3, d["lb_step"]["value"]))
+PY
