@@ -276,46 +276,68 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcn
 // LDS-only block barrier: the waves' global stores stay in flight.
 __device__ __forceinline__ void block_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// step() (:403-513) after the step counter advanced, for this lane's env held in registers:
-// action decode, table lookups, take_action (:578-686), reward (:516-567), next_request()
-// (:1131-1163).  Writes the endpoint words of the env's obs image (me) and returns the
-// reward.  ED_REGS: the history counters advance in ed[] (the multi-step rollout keeps them
-// in registers); otherwise the changed words are stored at once when keep is set.
-// STORED: the request node's zone comes from the node-zone words (nodes >= 64 from HBM)
-// instead of a redraw.
-// ED_REGS also keeps the observed latency / cpu of every endpoint in olat / ocpu (float32,
-// the obs columns): only the selected endpoint's change in a step, so the rollout gathers 4
-// table values per step instead of up to 2E + 4.
+// step() (:403-513) of this lane's env held in registers, in two parts.  tpe_prep: the
+// action's decode, the selected endpoint and the 4 table values take_action needs (they
+// depend only on the action and the counters, so a multi-step kernel issues them for the
+// next step while the current step's rows are being stored).
+struct TPrep {
+    int a, ai, oA, jA, Mn, jn;
+    bool accept, reject;
+    uint32_t emA, edA, edO;
+    double lat0A, lut_selA, sel_cpu, next_lat, next_cpu;
+};
+__device__ __forceinline__ TPrep tpe_prep(const Params& p, const double (&lat0)[TPE_E], const uint32_t (&em)[TPE_E],
+                                          const uint32_t (&ed)[TPE_E], int a) {
+    TPrep r;
+    const int E = p.E;
+    r.a = a;
+    r.accept = a >= -E && a < E;
+    r.reject = a == E;
+    r.ai = r.accept ? (a < 0 ? a + E : a) : 0;
+    r.emA = em[0];
+    r.edA = ed[0];
+    r.lat0A = lat0[0];
+#pragma unroll
+    for (int e = 1; e < TPE_E; ++e)
+        if (r.ai == e) { r.emA = em[e]; r.edA = ed[e]; r.lat0A = lat0[e]; }
+    r.oA = em_owner(r.emA);
+    r.edO = ed[0];
+#pragma unroll
+    for (int e = 1; e < TPE_E; ++e)
+        if (r.oA == e) r.edO = ed[e];
+    r.jA = ed_j(r.edA);
+    r.Mn = ed_M(r.edO) < CMAX ? ed_M(r.edO) + 1 : CMAX;
+    r.jn = r.jA < CMAX ? r.jA + 1 : CMAX;
+    const int k0A = (int)r.lat0A, c0A = em_c0(r.emA);
+    r.lut_selA = p.lat_lut[(r.jA) * LAT_ROWS + k0A];
+    r.sel_cpu = p.cpu_lut[(ed_m(r.edA)) * CPU_ROWS + c0A];
+    r.next_lat = p.lat_lut[(r.jn) * LAT_ROWS + k0A];
+    r.next_cpu = p.cpu_lut[(r.Mn) * CPU_ROWS + c0A];
+    return r;
+}
+
+// tpe_apply (after the step counter advanced): take_action (:578-686), reward (:516-567),
+// next_request() (:1131-1163).  Writes the endpoint words of the env's obs image (me) and
+// returns the reward.  ED_REGS: the history counters advance in ed[] (the multi-step
+// rollout keeps them in registers); otherwise the changed words are stored at once when
+// keep is set.  ED_REGS also keeps the observed latency / cpu of every endpoint in olat /
+// ocpu (float32, the obs columns): only the selected endpoint's change in a step, so the
+// rollout gathers 4 table values per step instead of up to 2E + 4.  STORED: the request
+// node's zone comes from the node-zone words (nodes >= 64 from HBM) instead of a redraw.
 template <bool TRACE, bool STORED, bool ED_REGS>
-__device__ __forceinline__ double tpe_step_core(const Params& p, int64_t ev, int64_t env, bool keep, TEnv& v,
-                                                const double (&lat0)[TPE_E], const uint32_t (&em)[TPE_E],
-                                                uint32_t (&ed)[TPE_E], float (&olat)[TPE_E], float (&ocpu)[TPE_E],
-                                                int a, uint32_t* me) {
+__device__ __forceinline__ double tpe_apply(const Params& p, const TPrep& pr, int64_t ev, int64_t env, bool keep,
+                                            TEnv& v, const double (&lat0)[TPE_E], const uint32_t (&em)[TPE_E],
+                                            uint32_t (&ed)[TPE_E], float (&olat)[TPE_E], float (&ocpu)[TPE_E],
+                                            uint32_t* me) {
     constexpr bool stored = STORED;
     const int E = p.E;
-    const bool accept = a >= -E && a < E;
-    const bool reject = a == E;
+    const int a = pr.a, ai = pr.ai, oA = pr.oA, jA = pr.jA, Mn = pr.Mn, jn = pr.jn;
+    const bool accept = pr.accept, reject = pr.reject;
+    const uint32_t emA = pr.emA, edA = pr.edA, edO = pr.edO;
+    const double lat0A = pr.lat0A, lut_selA = pr.lut_selA, sel_cpu = pr.sel_cpu, next_lat = pr.next_lat,
+                 next_cpu = pr.next_cpu;
     if (a < -E) v.s.bad = 1;  // reference: IndexError; here: treated as unrecognised
     if (!v.s.reset_done) v.s.bad = 1;
-    const int ai = accept ? (a < 0 ? a + E : a) : 0;
-    uint32_t emA = em[0], edA = ed[0];
-    double lat0A = lat0[0];
-#pragma unroll
-    for (int e = 1; e < TPE_E; ++e)
-        if (ai == e) { emA = em[e]; edA = ed[e]; lat0A = lat0[e]; }
-    const int oA = em_owner(emA);
-    uint32_t edO = ed[0];
-#pragma unroll
-    for (int e = 1; e < TPE_E; ++e)
-        if (oA == e) edO = ed[e];
-    const int jA = ed_j(edA);
-    const int Mn = ed_M(edO) < CMAX ? ed_M(edO) + 1 : CMAX;
-    const int jn = jA < CMAX ? jA + 1 : CMAX;
-    const int k0A = (int)lat0A, c0A = em_c0(emA);
-    const double lut_selA = p.lat_lut[(jA) * LAT_ROWS + k0A];
-    const double sel_cpu = p.cpu_lut[(ed_m(edA)) * CPU_ROWS + c0A];
-    const double next_lat = p.lat_lut[(jn) * LAT_ROWS + k0A];
-    const double next_cpu = p.cpu_lut[(Mn) * CPU_ROWS + c0A];
     int cnt = 0;  // #{e != ai : loads[e] <= loads[ai]} for the O(E) Gini update
 #pragma unroll
     for (int e = 0; e < TPE_E; ++e) {
@@ -481,8 +503,8 @@ __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
     const bool do_reset = done && p.auto_reset;
     const bool keep = live && !do_reset;  // the state stores reset() below does not redo
     float no_olat[TPE_E], no_ocpu[TPE_E];  // (unused: the single step gathers the observed values)
-    const double reward = tpe_step_core<TRACE, stored, false>(p, ev, env, keep, v, lat0, em, ed, no_olat, no_ocpu,
-                                                              a, me);
+    const TPrep pr = tpe_prep(p, lat0, em, ed, a);
+    const double reward = tpe_apply<TRACE, stored, false>(p, pr, ev, env, keep, v, lat0, em, ed, no_olat, no_ocpu, me);
     if (live) {
         if (p.reward) *(p.reward + env) = ((float)reward);
         if (p.done) p.done[env] = (uint8_t)done;
@@ -796,20 +818,24 @@ __global__ __launch_bounds__(NB) void k_rollout_tpe(Params p, int K, int32_t* ac
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
 
+    // step 0's action and table values; each later step's are issued at the end of the step
+    // before it, so their gathers are in flight while that step's rows are stored
+    // (PRE only: the in-loop block-list resets hold too many registers for it)
+    TPrep pr;
+    if constexpr (PRE) pr = tpe_prep(p, lat0, em, ed, tpe_policy<KIND>(p, ev, v, em, ed));
     for (int k = 0; k < K; ++k) {
+        if constexpr (!PRE) pr = tpe_prep(p, lat0, em, ed, tpe_policy<KIND>(p, ev, v, em, ed));
         uint4 q[10];  // the next episode's record, for an env this step ends
         if (pre && live && v.s.step + 1 == p.L) {
             const uint4* rp = p.rec + env * (RO_REC_BYTES / 16);
 #pragma unroll
             for (int j = 0; j < 10; ++j) q[j] = rp[j];
         }
-        const int a = tpe_policy<KIND>(p, ev, v, em, ed);
-        if (act_out && live) act_out[k * p.B + env] = a;
+        if (act_out && live) act_out[k * p.B + env] = pr.a;
         v.s.step = v.s.step < 0xFFFF ? v.s.step + 1 : 0xFFFF;
         const bool done = live && v.s.step == p.L;  // (:472)
         const bool do_reset = done && p.auto_reset;
-        const double reward =
-            tpe_step_core<false, true, true>(p, ev, env, false, v, lat0, em, ed, olat, ocpu, a, nullptr);
+        const double reward = tpe_apply<false, true, true>(p, pr, ev, env, false, v, lat0, em, ed, olat, ocpu, nullptr);
         if (live) {
             if (p.reward) p.reward[k * p.B + env] = (float)reward;
             if (p.done) p.done[k * p.B + env] = (uint8_t)done;
@@ -829,6 +855,7 @@ __global__ __launch_bounds__(NB) void k_rollout_tpe(Params p, int K, int32_t* ac
                 tpe_start_episode(p, q, v, lat0, em, ed, olat, ocpu);
                 new_episode = true;
             }
+            if (k + 1 < K) pr = tpe_prep(p, lat0, em, ed, tpe_policy<KIND>(p, ev, v, em, ed));
             tpe_obs_rows(p, mine, v, em, olat, ocpu);
             wave_lds_sync();
             if (obs_k) tpe_copy_rows(p, obs_k, wimg, env0, m, COPY_ALL);
