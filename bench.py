@@ -5,12 +5,12 @@ One bench "step" = one vector step of every env on every GPU: take_action + rewa
 next_request + get_state + auto-reset with the env's uniform random policy drawn on the
 device (the random policy of BASELINE configs 2/3, the same draws lb_policy(random)
 returns).  Observations, rewards and dones go into a T-deep device ring, the shape of PPO's
-rollout storage (ppo_deepset.py:136-143), so writes stream to HBM instead of sitting in the
-256 MB Infinity Cache; terminal observations and episode-statistics rows of finished envs
+rollout storage (ppo_deepset.py:136-143; T = 100 as SURVEY 8d sizes it), so writes stream to
+HBM instead of sitting in the 256 MB Infinity Cache; terminal observations and episode-statistics rows of finished envs
 are written too.  Env state is resident in HBM before timing.
 
 Two launch shapes run the same steps (bit for bit, tests/test_gpu_api.py):
-  --launch rollout (default): lb_rollout, K = T vector steps per launch (k_rollout_tpe),
+  --launch rollout (default): lb_rollout, K = T = 100 vector steps per launch (k_rollout_tpe),
       the env state in registers between the steps of a launch, every step's outputs in
       its ring slot -- the step-only workload of config 3 (no host policy in the loop);
   --launch step: one lb_step launch per vector step (k_step_tpe), the VecEnv.step() shape
@@ -72,11 +72,12 @@ def parse(argv):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
-    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=100)  # one ring cycle: every timed launch is a full one
     ap.add_argument("--envs", type=int, default=1 << 20, help="envs in total (per GPU with --weak)")
     ap.add_argument("--weak", action="store_true", help="--envs per GPU (weak scaling)")
     ap.add_argument("--config", default="default", choices=sorted(CONFIGS))
-    ap.add_argument("--ring", type=int, default=16, help="rollout ring depth (obs slots)")
+    ap.add_argument("--ring", type=int, default=100,
+                    help="rollout ring depth (obs slots; PPO's T = 100 storage, SURVEY 8d); lb_rollout launches fill it")
     ap.add_argument("--no-graph", action="store_true", help="launch every step eagerly")
     ap.add_argument("--launch", default="rollout", choices=("rollout", "step"),
                     help="rollout: K = ring steps per lb_rollout launch; step: one lb_step per step")
@@ -290,7 +291,8 @@ def main(argv=None):
     try:
         with open(pmc_path) as f:
             pmc = json.load(f)
-        if pmc.get("config") == args.config and pmc.get("envs") == B:
+        if (pmc.get("config") == args.config and pmc.get("envs") == B
+                and pmc.get("steps_per_launch", 1) == (T if args.launch == "rollout" else 1)):
             traffic = pmc.get("hbm_bytes_per_launch")  # per launch: T steps in rollout mode
     except (OSError, ValueError):
         pass

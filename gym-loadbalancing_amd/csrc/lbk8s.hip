@@ -556,8 +556,9 @@ int lb_rollout(void* state, const lb_config* cfg, int64_t num_envs, int32_t poli
         p.ep_stats = ep_stats_out;
         const bool small = num_envs <= SMALL_TPE_MAX_B;
         const dim3 grid(small ? (unsigned)((num_envs + 63) / 64) : env_blocks(num_envs)), block(small ? 64 : BLOCK);
-        // episodes longer than the launch: next episodes drawn before the first step
-        const bool pre = cfg->auto_reset && cfg->episode_length > steps;
+        // episodes at least as long as the launch (an env ends at most once in it): next
+        // episodes drawn before the first step
+        const bool pre = cfg->auto_reset && cfg->episode_length >= steps;
 #define LB_ROLLOUT_TPE_NB(NB_, KIND_)                                                                         \
         if (pre) hipLaunchKernelGGL((k_rollout_tpe<NB_, KIND_, true>), grid, block, 0, s, p, (int)steps, actions_out); \
         else hipLaunchKernelGGL((k_rollout_tpe<NB_, KIND_, false>), grid, block, 0, s, p, (int)steps, actions_out);

@@ -792,15 +792,15 @@ __global__ __launch_bounds__(NB) void k_rollout_tpe(Params p, int K, int32_t* ac
     }
     bool new_episode = false;  // the scenario arrays need writing back
     const int64_t obs_slot = p.B * (int64_t)p.R * 8;
-    // episodes longer than the launch end at most once per env in it: their next episode is
+    // episodes at least as long as the launch end at most once per env in it: their next episode is
     // drawn here, before the first step, into the env's record (RS_W lanes per env, every
     // finishing env of the wave in rounds of 8), and the step that ends one only reloads
     // the registers from it -- no barrier and no serial reset chain inside the step loop.
     // Shorter episodes take the in-loop block-list path below.
-    constexpr bool pre = PRE;  // (host: auto_reset && L > K)
+    constexpr bool pre = PRE;  // (host: auto_reset && L >= K: an env ending at step k ends next at k + L >= K)
     if (pre) {
         const int to_done = p.L - v.s.step;
-        const bool fin = live && to_done >= 1 && to_done <= K;
+        const bool fin = live && to_done >= 1 && to_done <= K;  // ends at step to_done - 1 of this launch
         const uint64_t fm = __ballot(fin);
         if (fin) {
             uint32_t* it = wreg + 2 * __popcll(fm & ((1ull << lane) - 1));

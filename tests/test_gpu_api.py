@@ -311,12 +311,13 @@ def test_rollout_equals_policy_plus_step(B, kw, geometry, kind):
 @pytest.mark.parametrize("B,kw", [(40000, dict(num_endpoints=6, reward_function="multi")), (70000, {}),
                                   (131072, dict(reward_function="latency"))])
 @pytest.mark.parametrize("kind", ["random", "endpoint_cpu"])
-@pytest.mark.parametrize("K,L", [(23, 9), (16, 20)])
+@pytest.mark.parametrize("K,L", [(23, 9), (16, 20), (20, 20)])
 def test_rollout_tpe_staggered_equals_policy_plus_step(B, kw, kind, K, L):
     """k_rollout_tpe with staggered episodes (1/L of the envs finish at every step, the
     bench's steady state): == K x (lb_policy + lb_step), bit for bit, including the terminal
     obs and the episode-stats rows.  L <= K: envs can finish twice in a launch (in-loop
-    block-list resets); L > K: next episodes drawn into records before the first step."""
+    block-list resets); L >= K: next episodes drawn into records before the first step
+    (L == K: every env ends exactly once per launch)."""
     from lbk8s import LBVecEnv
     envs = [LBVecEnv(B, seed=5, as_tensors=True, episode_length=L, geometry="tpe", **kw) for _ in range(2)]
     gid = torch.arange(B, device="cuda")

@@ -16,4 +16,4 @@ $T rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/rp4_$n -o run --outpu
 $T rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/rp5_$n -o run --output-format csv -- $CMD > gpurun_out/rp5_$n.log 2>&1 || exit 1
 for z in rp1 rp2 rp3 rp4 rp5; do python3 tools/pmc_sum.py gpurun_out/${z}_$n/run_counter_collection.csv k_rollout_tpe || true; done
 python3 tools/pmc_traffic.py gpurun_out/rp4_$n/run_counter_collection.csv gpurun_out/rp5_$n/run_counter_collection.csv \
-    --envs $n --out gpurun_out/pmc_traffic_rollout_$n.json
+    --envs $n --steps-per-launch 100 --out gpurun_out/pmc_traffic_rollout_$n.json

@@ -20,7 +20,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
  && PMC_MODE=rollout timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmcr_write_${TAG} -o run \
       --output-format csv -- python3 tools/pmc_probe.py > gpurun_out/pmcr_write_${TAG}.log 2>&1 \
  && python3 tools/pmc_traffic.py gpurun_out/pmcr_fetch_${TAG}/run_counter_collection.csv \
-      gpurun_out/pmcr_write_${TAG}/run_counter_collection.csv --out gpurun_out/pmc_traffic_rollout_${TAG}.json \
+      gpurun_out/pmcr_write_${TAG}/run_counter_collection.csv --steps-per-launch 100 --out gpurun_out/pmc_traffic_rollout_${TAG}.json \
  && cp gpurun_out/pmc_traffic_rollout_${TAG}.json profiles/pmc_traffic_rollout.json \
  && timeout -k 10 400 python bench.py > gpurun_out/bench_${TAG}.log 2>&1 \
  && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o run --output-format csv \

@@ -2,8 +2,8 @@
 """Workload for the rocprofv3 PMC passes: bench.py's timed step (2^20 default envs, the
 env's random policy drawn in the kernel, obs / reward / done ring of 16, episodes staggered
 so 1/episode_length of the envs end and auto-reset every step), 16 lb_step launches after
-the stagger setup (PMC_MODE=rollout: 8 lb_rollout launches of 16 steps, bench.py's default
-launch shape), then 3 torch copies of 1 GiB (known bytes: calibrates FETCH_SIZE /
+the stagger setup (PMC_MODE=rollout: 8 lb_rollout launches of 100 steps into a 100-deep ring, bench.py's
+default launch shape), then 3 torch copies of 1 GiB (known bytes: calibrates FETCH_SIZE /
 WRITE_SIZE)."""
 import os
 import sys
@@ -24,7 +24,8 @@ def main():
     from bench import CONFIGS
     B = int(os.environ.get("PMC_ENVS", 1 << 20))
     env = LBVecEnv(B, seed=0, as_tensors=True, **CONFIGS[cfg])
-    R, T = env.cfg.obs_rows, 16
+    rollout = os.environ.get("PMC_MODE") == "rollout"
+    R, T = env.cfg.obs_rows, (100 if rollout else 16)  # bench.py's ring; a rollout launch fills it
     ring = torch.empty((T, B, R, 8), dtype=torch.float32, device="cuda")
     rew = torch.empty((T, B), dtype=torch.float32, device="cuda")
     done = torch.empty((T, B), dtype=torch.uint8, device="cuda")
@@ -35,7 +36,7 @@ def main():
         env.step_device(None, obs_out=ring[0], reward_out=rew[0], done_out=done[0])
         env.reset_masked((gid % L) == r)
     torch.cuda.synchronize()
-    if os.environ.get("PMC_MODE") == "rollout":
+    if rollout:
         for i in range(8):
             env.rollout("random", T, obs_out=ring, reward_out=rew, done_out=done)
     else:
