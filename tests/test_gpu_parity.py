@@ -203,6 +203,52 @@ def test_config2_rollout_matches_oracle(oracle_mod):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("B,K", [(40000, 20), (70000, 20), (70000, 7)])
+def test_rollout_tpe_staggered_matches_oracle(oracle_mod, B, K):
+    """bench.py's default launch (k_rollout_tpe: K vector steps per launch, the env's random
+    policy, staggered episodes, next episodes drawn into records before the first step since
+    L >= K) against the C oracle stepping one vector step at a time, bit for bit: obs,
+    reward, done, terminal obs, and the state after the launches.  64-thread blocks (40,000
+    envs, geometry pinned to tpe) and 256-thread blocks with a partial last block (70,000)."""
+    import torch
+
+    from lbk8s import LBVecEnv
+    L, seed = 20, 99
+    cfg = dict(episode_length=L)
+    env = LBVecEnv(B, seed=seed, as_tensors=True, geometry="tpe", **cfg)
+    orc = oracle_mod.OracleBatch(cfg, B, trace=False, seed=seed)
+    orc.init()
+    np.testing.assert_array_equal(env.reset().cpu().numpy(), orc.reset())
+    gid = np.arange(B)
+    for r in range(1, L):  # bench.py's stagger
+        env.step_device(None)
+        orc.step(orc.policy_random())
+        m = (gid % L) == r
+        env.reset_masked(torch.from_numpy(m.astype(np.uint8)).cuda())
+        orc.reset(mask=m.astype(np.uint8))
+    R = env.cfg.obs_rows
+    obs = torch.empty((K, B, R, 8), dtype=torch.float32, device="cuda")
+    rew = torch.empty((K, B), dtype=torch.float32, device="cuda")
+    done = torch.empty((K, B), dtype=torch.uint8, device="cuda")
+    for launch in range(3):
+        env.rollout("random", K, obs_out=obs, reward_out=rew, done_out=done)
+        o, rw, d = obs.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy().astype(bool)
+        for k in range(K):
+            o2, r2, d2, t2, _ = orc.step(orc.policy_random())
+            st = launch * K + k
+            assert 0 < d[k].sum() < B
+            np.testing.assert_array_equal(rw[k], r2, err_msg=f"reward step {st}")
+            np.testing.assert_array_equal(d[k], d2, err_msg=f"done step {st}")
+            np.testing.assert_array_equal(o[k], o2, err_msg=f"obs step {st}")
+        last = d[K - 1]
+        np.testing.assert_array_equal(env.terminal_obs.cpu().numpy()[last], t2[last])
+    np.testing.assert_array_equal(env.field("avg_load_served").cpu().numpy(), orc.field("loads"))
+    np.testing.assert_array_equal(env.field("current_time").cpu().numpy(), orc.field("t"))
+    np.testing.assert_array_equal(env.field("endpoint_latency").cpu().numpy(), orc.field("ep_lat"))
+    assert env.status() == 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("B", [4096, 131072, (1 << 19) + 4096])
 def test_staggered_auto_reset_matches_oracle(oracle_mod, B):
     """Auto-reset with staggered episodes (1/L of the envs end every step, as in bench.py):
