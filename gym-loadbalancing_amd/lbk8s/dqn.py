@@ -90,13 +90,26 @@ class DeviceReplayBuffer:
         self.pos_t.zero_()
         self.pos_pp.zero_()
 
-    def sample(self, batch_size):
+    def _indices(self, batch_size):
         upper = self.size if self.full else self.pos
         dev = self.obs.device
         bi = torch.randint(0, upper, (batch_size,), device=dev, generator=self.gen)
         ei = torch.randint(0, self.n_envs, (batch_size,), device=dev, generator=self.gen)
+        return bi, ei
+
+    def sample(self, batch_size):
+        bi, ei = self._indices(batch_size)
         return (self.obs[bi, ei], self.actions[bi, ei][:, None], self.next_obs[bi, ei],
                 self.dones[bi, ei][:, None], self.rewards[bi, ei][:, None])
+
+    def sample_into(self, batch_size, out):
+        """sample() (the same draws, the same values) into the fixed buffers `out` = (obs,
+        actions, next_obs, dones, rewards) of a captured train step."""
+        bi, ei = self._indices(batch_size)
+        flat = bi * self.n_envs + ei
+        for src, dst in zip((self.obs, self.actions, self.next_obs, self.dones, self.rewards), out):
+            torch.index_select(src.reshape((-1,) + tuple(src.shape[2:])), 0, flat,
+                               out=dst.view((batch_size,) + tuple(src.shape[2:])))
 
 
 def dqn_loss(q_network, target_network, obs, actions, next_obs, rewards, dones, gamma):
@@ -112,7 +125,8 @@ class DQN_DeepSets:
     def __init__(self, env, seed=1, torch_deterministic=True, num_steps: int = 100, learning_rate=2.5e-4,
                  buffer_size=10000, gamma=0.99, tau=1.0, n_minibatches: int = 4, target_network_frequency=500,
                  batch_size=128, start_e=1, end_e=0.05, exploration_fraction=0.5, learning_starts=10000,
-                 train_frequency=10, device=None, log_fn=None, num_envs=None, tensorboard_log=None):
+                 train_frequency=10, device=None, log_fn=None, num_envs=None, tensorboard_log=None,
+                 train_graph=None):
         # num_envs / tensorboard_log: accepted for signature compatibility with
         # dqn_deepset.py:46-67 (the env's num_envs is used; there is no tensorboard writer)
         self.env = env
@@ -135,10 +149,17 @@ class DQN_DeepSets:
         if lbdist.is_multi():
             lbdist.broadcast_parameters(self.q_network)  # replicas start from rank 0's weights
         self.target_network = deepcopy(self.q_network)
+        # the train step (loss, backward, Adam) as a HIP graph replayed on fixed sample
+        # buffers: ~60 launches per train step otherwise, the host-bound part of config 5
+        self.train_graph = (self.device.type == "cuda") if train_graph is None else bool(train_graph)
         # on a HIP device, torch's fused Adam: one multi-tensor kernel per train step
         self.optimizer = optim.Adam(self.q_network.parameters(), lr=learning_rate,
                                     fused=(self.device.type == "cuda" and os.environ.get("LBK8S_FUSED_ADAM", "1") == "1")
-                                    or None)
+                                    or None, capturable=self.train_graph)
+        self._multi = lbdist.is_multi()
+        self._gflat = torch.zeros(sum(p.numel() for p in self.q_network.parameters()), device=self.device) \
+            if self._multi else None
+        self._tgraphs = None
         self.rb = DeviceReplayBuffer(buffer_size, self.num_envs, env.observation_space.shape, self.device, self.gen)
         self._act = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
         self._done_u8 = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
@@ -216,18 +237,100 @@ class DQN_DeepSets:
                 graphs[explore, parity] = g
         return graphs
 
-    def train_step(self, global_step):
-        obs, actions, next_obs, dones, rewards = self.rb.sample(self.batch_size)
-        loss, _, old_val = dqn_loss(self.q_network, self.target_network, obs, actions, next_obs, rewards, dones,
-                                    self.gamma)
-        self.optimizer.zero_grad()
+    def _train_backward(self, obs, actions, next_obs, dones, rewards):
+        """dqn_deepset.py:180-190: TD loss and its gradients; with several ranks the gradients
+        end packed in the flat bucket that the all_reduce averages."""
+        loss, _, _ = dqn_loss(self.q_network, self.target_network, obs, actions, next_obs, rewards, dones,
+                              self.gamma)
+        self.optimizer.zero_grad(set_to_none=not self.train_graph)
         loss.backward()
-        allreduce_gradients(self.q_network)
+        if self._multi and self.train_graph:
+            torch.cat([p.grad.reshape(-1) for p in self.q_network.parameters()], out=self._gflat)
+        return loss
+
+    def _train_apply(self):
+        if self._multi and self.train_graph:
+            self._gflat /= torch.distributed.get_world_size()
+            off = 0
+            for p in self.q_network.parameters():
+                n = p.numel()
+                p.grad.copy_(self._gflat[off:off + n].view_as(p))
+                off += n
         self.optimizer.step()
+
+    def _capture_train(self):
+        """Capture the train step on fixed sample buffers: one graph on one rank, two graphs
+        around the gradient all_reduce on several (as PPO's minibatch step).  The warm-up
+        steps are undone (parameters restored, Adam state zeroed) and draw nothing from the
+        sampling generator, so a graphed run trains exactly as an eager one."""
+        B, rb = self.batch_size, self.rb
+        obs_shape = tuple(rb.obs.shape[2:])
+        self._tstatic = (torch.zeros((B,) + obs_shape, device=self.device),
+                         torch.zeros((B, 1), dtype=torch.long, device=self.device),
+                         torch.zeros((B,) + obs_shape, device=self.device),
+                         torch.zeros((B, 1), device=self.device), torch.zeros((B, 1), device=self.device))
+        params = list(self.q_network.parameters())
+        snap = [p.detach().clone() for p in params]
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for _ in range(2):  # warm-up: allocates grads, Adam state, workspaces
+                self._train_backward(*self._tstatic)
+                self._allreduce()
+                self._train_apply()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        if self._multi:
+            ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(ga):
+                self._tloss = self._train_backward(*self._tstatic)
+            with torch.cuda.graph(gb):
+                self._train_apply()
+            self._tgraphs = (ga, gb)
+        else:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._tloss = self._train_backward(*self._tstatic)
+                self._train_apply()
+            self._tgraphs = (g,)
+        with torch.no_grad():
+            for p, q in zip(params, snap):
+                p.copy_(q)
+            for st in self.optimizer.state.values():
+                for v in st.values():
+                    if isinstance(v, torch.Tensor):
+                        v.zero_()
+        fused.invalidate(self.q_network)
+
+    def _allreduce(self):
+        if self._multi and self.train_graph:
+            lbdist.all_reduce_sum(self._gflat)
+
+    def train_step(self, global_step):
+        if self.train_graph:
+            if self._tgraphs is None:
+                self._capture_train()
+            self.rb.sample_into(self.batch_size, self._tstatic)
+            self._tgraphs[0].replay()
+            if len(self._tgraphs) > 1:
+                self._allreduce()  # eager collective on the current stream, between the two graphs
+                self._tgraphs[1].replay()
+            loss = self._tloss
+        else:
+            loss = self._train_backward(*self.rb.sample(self.batch_size))
+            allreduce_gradients(self.q_network)
+            self._train_apply()
+        # the fused forward's cached weight image of the q network is stale now: neither a
+        # replayed Adam step nor torch's fused Adam kernel moves the version counters it keys on
+        fused.invalidate(self.q_network)
         self.train_steps += 1
         if global_step % self.target_network_frequency == 0:
-            for tp, qp in zip(self.target_network.parameters(), self.q_network.parameters()):
-                tp.data.copy_(self.tau * qp.data + (1.0 - self.tau) * tp.data)
+            # (dqn_deepset.py:199-203) in place on the parameters themselves, so their version
+            # counters move and the fused forward's cached weight image of the target is rebuilt
+            # (writes through .data would leave that image stale)
+            with torch.no_grad():
+                for tp, qp in zip(self.target_network.parameters(), self.q_network.parameters()):
+                    tp.copy_(self.tau * qp + (1.0 - self.tau) * tp)
+            fused.invalidate(self.target_network)
         return loss
 
     def learn(self, total_timesteps: int = 500000):

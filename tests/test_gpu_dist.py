@@ -20,14 +20,16 @@ def _env():
     return env
 
 
-def test_ppo_two_ranks_graph_equals_eager(tmp_path):
-    """Averaged gradients keep the replicas identical, and the split-graph minibatch step
-    (graphs around the gradient all_reduce) computes the eager update."""
+@pytest.mark.parametrize("algo", ["ppo", "dqn"])
+def test_two_ranks_graph_equals_eager(tmp_path, algo):
+    """Averaged gradients keep the replicas identical, and the split-graph step (graphs
+    around the gradient all_reduce: PPO's minibatch step, DQN's train step) computes the
+    eager update."""
     from lbk8s.dist import free_port
     out = tmp_path / "res.json"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           os.path.join(REPO, "tests", "dist_ppo_worker.py"), str(out)]
+           os.path.join(REPO, "tests", "dist_ppo_worker.py"), str(out), algo]
     r = subprocess.run(cmd, env=_env(), capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(out.read_text())

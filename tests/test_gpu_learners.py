@@ -42,6 +42,30 @@ def test_dqn_learns_end_to_end():
     assert algo.episode_returns
 
 
+def test_dqn_graph_train_step_matches_eager():
+    """The HIP-graph train step (captured once on fixed sample buffers, replayed) trains as
+    the eager one: same samples (the capture draws nothing), same updates; and after the
+    hard target syncs the fused forward of the target network sees the synced weights
+    (the cached weight image is rebuilt, not the initial one)."""
+    from lbk8s import LBVecEnv, fused
+    from lbk8s.dqn import DQN_DeepSets
+    res = []
+    for graph in (False, True):
+        env = LBVecEnv(64, seed=4, as_tensors=True, episode_length=10)
+        algo = DQN_DeepSets(env, buffer_size=64 * 100, batch_size=64, learning_starts=50, train_frequency=5,
+                            target_network_frequency=100, seed=1, train_graph=graph)
+        assert algo.train_graph == graph
+        algo.learn(total_timesteps=300)
+        assert algo.train_steps == len([s for s in range(300) if s > 50 and s % 5 == 0])
+        res.append([p.detach().clone() for p in algo.q_network.parameters()])
+        x = torch.rand((256, 9, 8), device="cuda")
+        with torch.no_grad():
+            for net in (algo.q_network, algo.target_network):
+                torch.testing.assert_close(fused.q_forward(net, x), net.q_network(x), rtol=1e-4, atol=1e-4)
+    for a, b in zip(*res):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=2e-6)
+
+
 def test_ppo_graph_update_matches_eager():
     """The HIP-graph minibatch step (captured once, replayed) computes the eager update:
     two updates, so the second rollout must see the first update's weights (the fused

@@ -104,7 +104,8 @@ def main():
                    ep_return=ppo.episode_returns[-1] if ppo.episode_returns else None)
     else:
         from lbk8s.dqn import DQN_DeepSets
-        dqn = DQN_DeepSets(env, seed=1, learning_starts=min(100, args.warmup // 2), device=dev)
+        dqn = DQN_DeepSets(env, seed=1, learning_starts=min(100, args.warmup // 2), device=dev,
+                           train_graph=os.environ.get("LBK8S_DQN_TRAIN_GRAPH", "1") == "1")  # (A/B switch)
         dqn.learn(args.warmup)
         barrier_sync()
         t0 = time.perf_counter()
@@ -115,7 +116,7 @@ def main():
         out.update(metric="env-steps/s including DQN training (config 5)", value=env_steps / wall,
                    unit="env-steps/s", vector_steps=args.steps, train_steps=dqn.train_steps,
                    ms_per_vector_step=wall / args.steps * 1e3,
-                   buffer_slots_per_env=dqn.rb.size,
+                   buffer_slots_per_env=dqn.rb.size, train_graph=dqn.train_graph,
                    ep_return=dqn.episode_returns[-1] if dqn.episode_returns else None)
     if rank == 0:
         print(json.dumps(out), flush=True)
