@@ -6,10 +6,11 @@
 // envs/baselines.py (greedy policies :6-35).  Public ABI: include/lbk8s.h; design
 // notes: DESIGN.md.
 //
-// Two step kernels share one state representation (lbk8s_common.h):
-//   * E <= 8 : k_step_tpe   — one lane per env, LDS-staged coalesced obs (lbk8s_tpe.h)
-//   * E >  8 : k_step_slice — one W-lane slice per env (4 envs per wave up to E = 64),
-//                             lanes over endpoints (lbk8s_slice.h)
+// Two state layouts / kernel shapes share one state representation (lbk8s_common.h):
+//   * E <= 8 : k_step_tpe    — one lane per env, LDS-staged coalesced obs (lbk8s_tpe.h);
+//              k_rollout_tpe — K steps per launch, the env in registers (lb_rollout)
+//   * E >  8 : k_step_slice  — one W-lane slice per env (4 envs per wave up to E = 64),
+//                              lanes over endpoints; k_rollout_slice (lbk8s_slice.h)
 
 #include <hip/hip_runtime.h>
 
