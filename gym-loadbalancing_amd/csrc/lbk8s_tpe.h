@@ -269,6 +269,54 @@ __global__ __launch_bounds__(NB) void k_reset_tpe(Params p) {
     if (p.obs) tpe_copy_out(p, p.obs, img, env0, COPY_FLAGGED);
 }
 
+constexpr int RO_STRIDE = 19;  // float4 per lane in the rollout's obs image (2R <= 18, + 1 pad)
+constexpr int RO_REC_OFF = 512;  // words: a wave region's reset records, past its list (<= 449 words)
+// lanes per reset in the rollout: a whole wave per finishing env (the 24 node draws, 8
+// endpoint draws and the request in parallel, a chain about 3 Philox blocks deep), each of
+// the block's waves takes one listed env per round.  With staggered episodes a 256-env
+// block has ~2.6 finishing envs per step: 8-lane groups left three waves parked at the
+// barrier behind one wave's 5-block-deep reset chain (2^20 envs: 111 us per step vs 78
+// lockstep).
+constexpr int RO_RW = 64;
+
+// get_state() (:688-758) rows of this lane's env from registers, into its LDS image
+__device__ __forceinline__ void tpe_obs_rows(const Params& p, float4* row, const TEnv& v,
+                                             const uint32_t (&em)[TPE_E], const float (&olat)[TPE_E],
+                                             const float (&ocpu)[TPE_E]) {
+    const float rz = (float)v.s.rz, thr = (float)threshold(v.s.thr_idx), dt = (float)v.dt;
+#pragma unroll
+    for (int e = 0; e < TPE_E; ++e) {
+        if (e < p.E) {
+            const int z = em_zone(em[e]);
+            row[2 * e] = make_float4((float)z, (float)zcap_val(v.zcap, z), ocpu[e], (float)topo_val(v.topo, z, v.s.rz));
+            row[2 * e + 1] = make_float4(olat[e], rz, thr, dt);
+        }
+    }
+    if (p.R > p.E) {  // the reject row
+        row[2 * p.E] = make_float4(-1.f, -1.f, -1.f, -1.f);
+        row[2 * p.E + 1] = make_float4(-1.f, rz, thr, dt);
+    }
+}
+
+// envs el0 .. el0 + nstage - 1 of the wave from its image (lane el - el0 holds env el's rows)
+// as contiguous float4 runs (G envs per store instruction); m = the wave's finishing envs,
+// which = COPY_ALL / FLAGGED / UNFLAGGED
+__device__ __forceinline__ void tpe_copy_rows(const Params& p, float* out, const float4* wimg, int64_t env0,
+                                              uint64_t m, int which, int el0, int nstage) {
+    const int lane = threadIdx.x & 63;
+    const int P = 2 * p.R;
+    const int G = 64 / P;
+    const int eo = lane / P, piece = lane - eo * P;
+    if (eo >= G) return;
+    const int64_t left = p.B - env0;
+    const int nenv = left < el0 + nstage ? (int)left : el0 + nstage;
+    float4* base = reinterpret_cast<float4*>(out + env0 * (int64_t)p.R * 8) + piece;
+    for (int el = el0 + eo; el < nenv; el += G) {
+        if (which != COPY_ALL && (which == COPY_FLAGGED) != (((m >> el) & 1) != 0)) continue;
+        st_stream(base + el * P, wimg[(el - el0) * RO_STRIDE + piece]);
+    }
+}
+
 // The LDS image and the copy-out are wave-local: a wave orders its own LDS accesses, so it
 // needs no block barrier (which would also wait for every global store the wave has in
 // flight); the compiler is kept from moving LDS accesses across the point.
@@ -324,7 +372,7 @@ __device__ __forceinline__ TPrep tpe_prep(const Params& p, const double (&lat0)[
 // ocpu (float32, the obs columns): only the selected endpoint's change in a step, so the
 // rollout gathers 4 table values per step instead of up to 2E + 4.  STORED: the request
 // node's zone comes from the node-zone words (nodes >= 64 from HBM) instead of a redraw.
-template <bool TRACE, bool STORED, bool ED_REGS>
+template <bool TRACE, bool STORED, bool ED_REGS, bool OBS_REGS = ED_REGS>
 __device__ __forceinline__ double tpe_apply(const Params& p, const TPrep& pr, int64_t ev, int64_t env, bool keep,
                                             TEnv& v, const double (&lat0)[TPE_E], const uint32_t (&em)[TPE_E],
                                             uint32_t (&ed)[TPE_E], float (&olat)[TPE_E], float (&ocpu)[TPE_E],
@@ -349,7 +397,7 @@ __device__ __forceinline__ double tpe_apply(const Params& p, const TPrep& pr, in
             if constexpr (ED_REGS) {
                 ol = olat[e];
                 oc = ocpu[e];
-            } else {
+            } else {  // (the single step gathers the observed values of every endpoint)
                 const int m = ed_m(ed[e]);
                 double l = lat0[e], c = (double)em_c0(em[e]);
                 if (j) l = p.lat_lut[j * LAT_ROWS + (int)lat0[e]];
@@ -358,7 +406,7 @@ __device__ __forceinline__ double tpe_apply(const Params& p, const TPrep& pr, in
                 oc = (float)c;
             }
             if (accept && e == ai) { ol = (float)next_lat; oc = (float)next_cpu; }
-            if constexpr (ED_REGS) {  // (the caller writes the obs rows from olat / ocpu)
+            if constexpr (OBS_REGS) {  // (the caller writes the obs rows from olat / ocpu)
                 olat[e] = ol;
                 ocpu[e] = oc;
             } else {
@@ -448,12 +496,17 @@ __device__ __forceinline__ double tpe_apply(const Params& p, const TPrep& pr, in
 // profiles/r01_ablation.jsonl): 131,072 envs 25.4 -> 23.9 us per step, 2^19 67 -> 64.5,
 // 2^20 equal (112 us): the second launch's ramp, not the reset work, was the cost.
 constexpr int RS_LIST_W = 7;  // words per list item: env, t (2), acc3 (2), sc (2)
+constexpr int STEP_STAGE = 32;  // k_step_tpe: envs per obs staging pass (half a wave)
 template <bool TRACE, bool RECOMPUTE, int NB = BLOCK>
 __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
-    __shared__ uint32_t lds[NB * TPE_CW];
-    const int lane = threadIdx.x & 63;
-    uint32_t* img = lds + (threadIdx.x & ~63) * TPE_CW;
-    uint32_t* me = img + lane * TPE_CW;
+    constexpr int NW = NB / 64;
+    // per wave: half the wave's finished (R x 8) rows at a time (the list of finishing envs
+    // reuses the region); 39 KB per 256-thread block keeps 4 blocks per CU
+    __shared__ float4 oimg[NW][STEP_STAGE * RO_STRIDE];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float4* wimg = oimg[wv];
+    uint32_t* img = reinterpret_cast<uint32_t*>(wimg);
+    float4* mine = wimg + (lane % STEP_STAGE) * RO_STRIDE;
     const int64_t env0 = (int64_t)blockIdx.x * NB + (threadIdx.x & ~63);
     const int64_t env = env0 + lane;
     const bool live = env < p.B;
@@ -502,27 +555,30 @@ __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
     const bool done = live && v.s.step == p.L;  // (:472)
     const bool do_reset = done && p.auto_reset;
     const bool keep = live && !do_reset;  // the state stores reset() below does not redo
-    float no_olat[TPE_E], no_ocpu[TPE_E];  // (unused: the single step gathers the observed values)
+    float olat[TPE_E], ocpu[TPE_E];  // observed endpoint latency / cpu after the step
     const TPrep pr = tpe_prep(p, lat0, em, ed, a);
-    const double reward = tpe_apply<TRACE, stored, false>(p, pr, ev, env, keep, v, lat0, em, ed, no_olat, no_ocpu, me);
+    const double reward = tpe_apply<TRACE, stored, false, true>(p, pr, ev, env, keep, v, lat0, em, ed, olat, ocpu,
+                                                                nullptr);
     if (live) {
         if (p.reward) *(p.reward + env) = ((float)reward);
         if (p.done) p.done[env] = (uint8_t)done;
     }
-    tpe_image_env(me, v, do_reset ? TPE_FLAG : 0);
 
     // ---- VecEnv auto-reset: terminal obs + episode stats, then reset() below
     const uint64_t m = __ballot(do_reset);
     if (do_reset && p.ep_stats)
         write_stats_row(p, p.ep_stats + env * LB_ST_K, v.s, v.acc2, v.acc3, v.total, v.sum_lat, v.sum_cpu);
     if (keep) tpe_store_scalars(p, env, v);
-    wave_lds_sync();
-    if (p.term_obs && m) tpe_copy_out(p, p.term_obs, img, env0, COPY_FLAGGED);
-    // finished envs' post-reset obs come from their reset()
-    if (p.obs) tpe_copy_out(p, p.obs, img, env0, p.auto_reset ? COPY_UNFLAGGED : COPY_ALL);
-    if (p.auto_reset) {  // uniform over the grid: every wave reaches the barrier
-        constexpr int NW = NB / 64;
+    // get_state() rows built once per env, staged half a wave at a time; the finished envs'
+    // post-reset obs come from their reset()
+    for (int el0 = 0; el0 < 64; el0 += STEP_STAGE) {
+        if (lane / STEP_STAGE == el0 / STEP_STAGE) tpe_obs_rows(p, mine, v, em, olat, ocpu);
         wave_lds_sync();
+        if (p.term_obs && m) tpe_copy_rows(p, p.term_obs, wimg, env0, m, COPY_FLAGGED, el0, STEP_STAGE);
+        if (p.obs) tpe_copy_rows(p, p.obs, wimg, env0, m, p.auto_reset ? COPY_UNFLAGGED : COPY_ALL, el0, STEP_STAGE);
+        wave_lds_sync();
+    }
+    if (p.auto_reset) {  // uniform over the grid: every wave reaches the barrier
         if (do_reset) {  // the wave's list replaces its (copied-out) image
             uint32_t* it = img + 1 + RS_LIST_W * __popcll(m & ((1ull << lane) - 1));
             const uint64_t tb = (uint64_t)__double_as_longlong(v.t), sc = sc_pack(v.s);
@@ -537,8 +593,8 @@ __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
         int pre[NW + 1];
         pre[0] = 0;
 #pragma unroll
-        for (int w = 0; w < NW; ++w) pre[w + 1] = pre[w] + (int)lds[w * 64 * TPE_CW];
-        const int wv = threadIdx.x >> 6, g = lane / RS_W, gl = lane % RS_W;
+        for (int w = 0; w < NW; ++w) pre[w + 1] = pre[w] + (int)reinterpret_cast<const uint32_t*>(oimg[w])[0];
+        const int g = lane / RS_W, gl = lane % RS_W;
         for (int i = wv * (64 / RS_W) + g; i < pre[NW]; i += NW * (64 / RS_W)) {
             int q = 0;
 #pragma unroll
@@ -546,7 +602,7 @@ __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
             int base = 0;
 #pragma unroll
             for (int w = 1; w < NW; ++w) base = q == w ? pre[w] : base;
-            const uint32_t* it = lds + q * 64 * TPE_CW + 1 + RS_LIST_W * (i - base);
+            const uint32_t* it = reinterpret_cast<const uint32_t*>(oimg[q]) + 1 + RS_LIST_W * (i - base);
             const int64_t renv = (int64_t)it[0];
             SEnv<1> sv;
             sv.t = __longlong_as_double((long long)((uint64_t)it[1] | ((uint64_t)it[2] << 32)));
@@ -603,53 +659,6 @@ __device__ __forceinline__ int tpe_policy(const Params& p, int64_t ev, const TEn
 // between steps, so no barrier waits on global stores.  Needs N <= 64 (the node-zone words
 // stay in registers).  Bit for bit K x (lb_policy + lb_step) (tests/test_gpu_api.py).
 constexpr int RS_REC_W = 40;   // LDS record of a reset: lat0 (16), emeta (8), topo, zcap, nz0, nz1, t, acc3, sc
-constexpr int RO_STRIDE = 19;  // float4 per lane in the rollout's obs image (2R <= 18, + 1 pad)
-constexpr int RO_REC_OFF = 512;  // words: a wave region's reset records, past its list (<= 449 words)
-// lanes per reset in the rollout: a whole wave per finishing env (the 24 node draws, 8
-// endpoint draws and the request in parallel, a chain about 3 Philox blocks deep), each of
-// the block's waves takes one listed env per round.  With staggered episodes a 256-env
-// block has ~2.6 finishing envs per step: 8-lane groups left three waves parked at the
-// barrier behind one wave's 5-block-deep reset chain (2^20 envs: 111 us per step vs 78
-// lockstep).
-constexpr int RO_RW = 64;
-
-// get_state() (:688-758) rows of this lane's env from registers, into its LDS image
-__device__ __forceinline__ void tpe_obs_rows(const Params& p, float4* row, const TEnv& v,
-                                             const uint32_t (&em)[TPE_E], const float (&olat)[TPE_E],
-                                             const float (&ocpu)[TPE_E]) {
-    const float rz = (float)v.s.rz, thr = (float)threshold(v.s.thr_idx), dt = (float)v.dt;
-#pragma unroll
-    for (int e = 0; e < TPE_E; ++e) {
-        if (e < p.E) {
-            const int z = em_zone(em[e]);
-            row[2 * e] = make_float4((float)z, (float)zcap_val(v.zcap, z), ocpu[e], (float)topo_val(v.topo, z, v.s.rz));
-            row[2 * e + 1] = make_float4(olat[e], rz, thr, dt);
-        }
-    }
-    if (p.R > p.E) {  // the reject row
-        row[2 * p.E] = make_float4(-1.f, -1.f, -1.f, -1.f);
-        row[2 * p.E + 1] = make_float4(-1.f, rz, thr, dt);
-    }
-}
-
-// the wave's envs' rows from its image as contiguous float4 runs (G envs per store
-// instruction); m = the wave's finishing envs, which = COPY_ALL / FLAGGED / UNFLAGGED
-__device__ __forceinline__ void tpe_copy_rows(const Params& p, float* out, const float4* wimg, int64_t env0,
-                                              uint64_t m, int which) {
-    const int lane = threadIdx.x & 63;
-    const int P = 2 * p.R;
-    const int G = 64 / P;
-    const int eo = lane / P, piece = lane - eo * P;
-    if (eo >= G) return;
-    const int64_t left = p.B - env0;
-    const int nenv = left < 64 ? (int)left : 64;
-    float4* base = reinterpret_cast<float4*>(out + env0 * (int64_t)p.R * 8) + piece;
-    for (int el = eo; el < nenv; el += G) {
-        if (which != COPY_ALL && (which == COPY_FLAGGED) != (((m >> el) & 1) != 0)) continue;
-        st_stream(base + el * P, wimg[el * RO_STRIDE + piece]);
-    }
-}
-
 // The next episode of an env, as reset() (:290-400) draws it in Philox mode, into its
 // RO_REC_BYTES record (p.rec): W lanes per env, lane e < E its endpoint (the same draws and
 // owner rule as slice_reset).  Words: lat0 [0,16), emeta [16,24), topo, zcap, nz0, nz1, the
@@ -848,7 +857,7 @@ __global__ __launch_bounds__(NB) void k_rollout_tpe(Params p, int K, int32_t* ac
             if (p.term_obs && m) {  // the finishing envs' terminal rows first
                 if (do_reset) tpe_obs_rows(p, mine, v, em, olat, ocpu);
                 wave_lds_sync();
-                tpe_copy_rows(p, p.term_obs, wimg, env0, m, COPY_FLAGGED);
+                tpe_copy_rows(p, p.term_obs, wimg, env0, m, COPY_FLAGGED, 0, 64);
                 wave_lds_sync();
             }
             if (do_reset) {
@@ -858,13 +867,13 @@ __global__ __launch_bounds__(NB) void k_rollout_tpe(Params p, int K, int32_t* ac
             if (k + 1 < K) pr = tpe_prep(p, lat0, em, ed, tpe_policy<KIND>(p, ev, v, em, ed));
             tpe_obs_rows(p, mine, v, em, olat, ocpu);
             wave_lds_sync();
-            if (obs_k) tpe_copy_rows(p, obs_k, wimg, env0, m, COPY_ALL);
+            if (obs_k) tpe_copy_rows(p, obs_k, wimg, env0, m, COPY_ALL, 0, 64);
             continue;
         }
         tpe_obs_rows(p, mine, v, em, olat, ocpu);
         wave_lds_sync();
-        if (p.term_obs && m) tpe_copy_rows(p, p.term_obs, wimg, env0, m, COPY_FLAGGED);
-        if (obs_k) tpe_copy_rows(p, obs_k, wimg, env0, m, p.auto_reset ? COPY_UNFLAGGED : COPY_ALL);
+        if (p.term_obs && m) tpe_copy_rows(p, p.term_obs, wimg, env0, m, COPY_FLAGGED, 0, 64);
+        if (obs_k) tpe_copy_rows(p, obs_k, wimg, env0, m, p.auto_reset ? COPY_UNFLAGGED : COPY_ALL, 0, 64);
         if (!p.auto_reset) continue;  // uniform over the grid
         wave_lds_sync();
         if (do_reset) {  // the wave's list replaces its (copied-out) image
