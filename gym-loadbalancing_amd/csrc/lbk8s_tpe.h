@@ -333,7 +333,14 @@ struct TPrep {
     bool accept, reject;
     uint32_t emA, edA, edO;
     double lat0A, lut_selA, sel_cpu, next_lat, next_cpu;
+    double x1, x2;  // the step's next_request() draws (tpe_prep_request; Philox mode)
+    int r, n;
 };
+// the draws of the next_request() that closes the coming step (slot = its step count)
+__device__ __forceinline__ void tpe_prep_request(const Params& p, int64_t ev, const TEnv& v, TPrep& pr) {
+    const int slot = v.s.step < 0xFFFF ? v.s.step + 1 : 0xFFFF;
+    tpe_request_draws<false>(p, ev, (uint32_t)(v.acc3 >> 32), (uint32_t)slot, false, pr.x1, pr.x2, pr.r, pr.n);
+}
 __device__ __forceinline__ TPrep tpe_prep(const Params& p, const double (&lat0)[TPE_E], const uint32_t (&em)[TPE_E],
                                           const uint32_t (&ed)[TPE_E], int a) {
     TPrep r;
@@ -372,7 +379,7 @@ __device__ __forceinline__ TPrep tpe_prep(const Params& p, const double (&lat0)[
 // ocpu (float32, the obs columns): only the selected endpoint's change in a step, so the
 // rollout gathers 4 table values per step instead of up to 2E + 4.  STORED: the request
 // node's zone comes from the node-zone words (nodes >= 64 from HBM) instead of a redraw.
-template <bool TRACE, bool STORED, bool ED_REGS, bool OBS_REGS = ED_REGS>
+template <bool TRACE, bool STORED, bool ED_REGS, bool OBS_REGS = ED_REGS, bool REQ_PREP = false>
 __device__ __forceinline__ double tpe_apply(const Params& p, const TPrep& pr, int64_t ev, int64_t env, bool keep,
                                             TEnv& v, const double (&lat0)[TPE_E], const uint32_t (&em)[TPE_E],
                                             uint32_t (&ed)[TPE_E], float (&olat)[TPE_E], float (&ocpu)[TPE_E],
@@ -465,7 +472,11 @@ __device__ __forceinline__ double tpe_apply(const Params& p, const TPrep& pr, in
     {
         double x1, x2;
         int r, n;
-        tpe_request_draws<TRACE>(p, ev, (uint32_t)(v.acc3 >> 32), (uint32_t)v.s.step, false, x1, x2, r, n);
+        if constexpr (REQ_PREP) {
+            x1 = pr.x1; x2 = pr.x2; r = pr.r; n = pr.n;
+        } else {
+            tpe_request_draws<TRACE>(p, ev, (uint32_t)(v.acc3 >> 32), (uint32_t)v.s.step, false, x1, x2, r, n);
+        }
         const double arrival = v.t + x1;
         const double departure = arrival + x2;
         v.dt = departure - arrival;
@@ -831,7 +842,10 @@ __global__ __launch_bounds__(NB) void k_rollout_tpe(Params p, int K, int32_t* ac
     // before it, so their gathers are in flight while that step's rows are stored
     // (PRE only: the in-loop block-list resets hold too many registers for it)
     TPrep pr;
-    if constexpr (PRE) pr = tpe_prep(p, lat0, em, ed, tpe_policy<KIND>(p, ev, v, em, ed));
+    if constexpr (PRE) {
+        pr = tpe_prep(p, lat0, em, ed, tpe_policy<KIND>(p, ev, v, em, ed));
+        tpe_prep_request(p, ev, v, pr);
+    }
     for (int k = 0; k < K; ++k) {
         if constexpr (!PRE) pr = tpe_prep(p, lat0, em, ed, tpe_policy<KIND>(p, ev, v, em, ed));
         uint4 q[10];  // the next episode's record, for an env this step ends
@@ -844,7 +858,8 @@ __global__ __launch_bounds__(NB) void k_rollout_tpe(Params p, int K, int32_t* ac
         v.s.step = v.s.step < 0xFFFF ? v.s.step + 1 : 0xFFFF;
         const bool done = live && v.s.step == p.L;  // (:472)
         const bool do_reset = done && p.auto_reset;
-        const double reward = tpe_apply<false, true, true>(p, pr, ev, env, false, v, lat0, em, ed, olat, ocpu, nullptr);
+        const double reward =
+            tpe_apply<false, true, true, true, PRE>(p, pr, ev, env, false, v, lat0, em, ed, olat, ocpu, nullptr);
         if (live) {
             if (p.reward) p.reward[k * p.B + env] = (float)reward;
             if (p.done) p.done[k * p.B + env] = (uint8_t)done;
@@ -864,7 +879,10 @@ __global__ __launch_bounds__(NB) void k_rollout_tpe(Params p, int K, int32_t* ac
                 tpe_start_episode(p, q, v, lat0, em, ed, olat, ocpu);
                 new_episode = true;
             }
-            if (k + 1 < K) pr = tpe_prep(p, lat0, em, ed, tpe_policy<KIND>(p, ev, v, em, ed));
+            if (k + 1 < K) {
+                pr = tpe_prep(p, lat0, em, ed, tpe_policy<KIND>(p, ev, v, em, ed));
+                tpe_prep_request(p, ev, v, pr);
+            }
             tpe_obs_rows(p, mine, v, em, olat, ocpu);
             wave_lds_sync();
             if (obs_k) tpe_copy_rows(p, obs_k, wimg, env0, m, COPY_ALL, 0, 64);
