@@ -662,14 +662,20 @@ __device__ __forceinline__ int tpe_policy(const Params& p, int64_t ev, const TEn
 // banks), and the wave copies its 64 envs' rows out as contiguous float4 runs; building
 // the rows once per env instead of decoding a compact image per stored piece took the
 // copy-out from about half of the step's VALU instructions to a load and a store.
-// Auto-reset: each wave lists its finishing envs in its image region (as k_step_tpe), and
-// after an LDS-only block barrier the block's waves run the listed resets RO_RW = 64 lanes
-// per env, one env per wave per round; a reset writes the env's post-reset obs into slot k and its
-// new episode (scenario, clock, request) into an LDS record, from which the owning lane
-// reloads its registers after a second barrier.  Nothing but the outputs leaves the CU
-// between steps, so no barrier waits on global stores.  Needs N <= 64 (the node-zone words
-// stay in registers).  Bit for bit K x (lb_policy + lb_step) (tests/test_gpu_api.py).
-constexpr int RS_REC_W = 40;   // LDS record of a reset: lat0 (16), emeta (8), topo, zcap, nz0, nz1, t, acc3, sc
+// Auto-reset, PRE (episode_length >= K, so an env ends at most once per launch; the bench's
+// L = K = 100): before the first step each wave draws the next episode of its envs that end
+// inside the launch into their records (tpe_write_record, 8 lanes per env); the step that
+// ends an episode loads the record at its start and starts the new episode from it
+// (tpe_start_episode) -- no barrier and no reset chain inside the step loop.  Otherwise
+// (L < K): each wave lists its finishing envs in its image region (as k_step_tpe), and after
+// an LDS-only block barrier the block's waves run the listed resets RO_RW = 64 lanes per env,
+// one env per wave per round; a reset writes the env's post-reset obs into slot k and its new
+// episode into an LDS record (RS_REC_W words), from which the owning lane reloads its
+// registers after a second barrier.  Nothing but the outputs leaves the CU between steps, so
+// no barrier waits on global stores.  Needs N <= 64 (the node-zone words stay in registers).
+// Bit for bit K x (lb_policy + lb_step) and the C oracle (tests/test_gpu_api.py,
+// tests/test_gpu_parity.py).
+constexpr int RS_REC_W = 40;   // LDS record of an in-loop reset: lat0 (16), emeta (8), topo, zcap, nz0, nz1, t, acc3, sc
 // The next episode of an env, as reset() (:290-400) draws it in Philox mode, into its
 // RO_REC_BYTES record (p.rec): W lanes per env, lane e < E its endpoint (the same draws and
 // owner rule as slice_reset).  Words: lat0 [0,16), emeta [16,24), topo, zcap, nz0, nz1, the
