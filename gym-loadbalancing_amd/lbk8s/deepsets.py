@@ -163,13 +163,18 @@ class DeepSetAgent(nn.Module):
         return action, dist.log_prob(action), dist.entropy(), value
 
     @torch.no_grad()
-    def act(self, x, masks=None, generator=None):
-        """Rollout step: (action, log_prob, value) with no autograd graph."""
+    def act(self, x, masks=None, generator=None, uniforms=None):
+        """Rollout step: (action, log_prob, value) with no autograd graph.  `uniforms` (B,)
+        U(0,1) draws: the categorical sample by inverse CDF on them (no RNG call inside, so
+        the step can be captured in a HIP graph); otherwise torch.multinomial."""
         from . import fused
         logits, value = fused.deepsets_forward(self, x)
         lg = masked_logits(logits, masks)
         logp_all = torch.log_softmax(lg, dim=-1)
-        if generator is None:
+        if uniforms is not None:
+            c = logp_all.exp().cumsum(dim=-1)
+            action = (c < uniforms[:, None] * c[:, -1:]).sum(dim=-1).clamp_(max=c.shape[-1] - 1)
+        elif generator is None:
             action = torch.multinomial(logp_all.exp(), 1).squeeze(-1)
         else:
             action = torch.multinomial(logp_all.exp(), 1, generator=generator).squeeze(-1)
