@@ -324,7 +324,14 @@ def main(argv=None):
                      # of the kernel is launch_ms; traffic is HBM bytes per launch (PMC)
                      "launch_ms": kernel_ms * (T if args.launch == "rollout" else 1),
                      "traffic_bytes_per_env_step": (traffic / B / (T if args.launch == "rollout" else 1)
-                                                    if traffic is not None else None)},
+                                                    if traffic is not None else None),
+                     # the same time against SURVEY 8(d)'s per-env-step bytes of the one-launch-
+                     # per-step design (the rollout moves fewer: frac > 1 there means it beats
+                     # that design's bandwidth bound), and against the PMC-measured bytes
+                     "frac_at_survey_bytes": b_step * B / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "frac_measured_traffic": (traffic / (T if args.launch == "rollout" else 1)
+                                               / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                               if traffic is not None else None)},
     }
     if step_res is not None:
         ks = step_res["kernel_ms"]
