@@ -146,6 +146,30 @@ def test_state_dict_names_match_reference():
     assert sum(p.numel() for p in DeepSetAgent(8).critic.parameters()) == 21633
 
 
+def test_rollout_sampler_is_the_categorical_distribution():
+    """DeepSetAgent.act(uniforms=...) (the PPO rollout's inverse-CDF sampler on pre-drawn
+    uniforms, ppo_deepset.py:169's Categorical.sample()): action frequencies follow the
+    softmax of the (masked) logits, masked actions (logit -1e8) are never taken, and the
+    log-prob is that of the taken action."""
+    from lbk8s.deepsets import DeepSetAgent
+    torch.manual_seed(0)
+    agent = DeepSetAgent(8)
+    n = 200_000
+    x = torch.rand(1, 9, 8).expand(n, 9, 8).contiguous()
+    masks = torch.ones(n, 9, dtype=torch.bool)
+    masks[:, 2] = False
+    masks[:, 7] = False
+    g = torch.Generator().manual_seed(1)
+    u = torch.rand(n, generator=g)
+    a, lp, _ = agent.act(x, masks, uniforms=u)
+    assert not bool(((a == 2) | (a == 7)).any())
+    with torch.no_grad():
+        p = torch.softmax(torch.where(masks[0], agent.actor(x[:1])[0], torch.tensor(-1e8)), dim=-1)
+    freq = torch.bincount(a, minlength=9).double() / n
+    assert torch.allclose(freq, p.double(), atol=4e-3), (freq, p)
+    torch.testing.assert_close(lp, torch.log(p)[a], rtol=1e-5, atol=1e-6)
+
+
 def test_gae_matches_direct_recursion():
     from lbk8s.ppo import compute_gae
     g = torch.Generator().manual_seed(0)
