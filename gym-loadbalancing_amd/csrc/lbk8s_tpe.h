@@ -734,7 +734,8 @@ __device__ __forceinline__ void tpe_write_record(const Params& p, int64_t env, u
 
 // reset() from the env's record: the episode counter advances, the clock runs on (t is
 // never reset, :1135), the first request arrives at t + x1
-// (q: the record's first 38 words, loaded at the start of the step so the load overlaps it)
+// (q: the record's first 38 words; loaded where the episode starts: loading them at the
+// start of the step held 40 more registers across it, 2^20: 67.5 -> 66.2 us per step)
 __device__ __forceinline__ void tpe_start_episode(const Params& p, const uint4 (&q)[10], TEnv& v,
                                                   double (&lat0)[TPE_E], uint32_t (&em)[TPE_E],
                                                   uint32_t (&ed)[TPE_E], float (&olat)[TPE_E],
@@ -854,12 +855,6 @@ __global__ __launch_bounds__(NB) void k_rollout_tpe(Params p, int K, int32_t* ac
     }
     for (int k = 0; k < K; ++k) {
         if constexpr (!PRE) pr = tpe_prep(p, lat0, em, ed, tpe_policy<KIND>(p, ev, v, em, ed));
-        uint4 q[10];  // the next episode's record, for an env this step ends
-        if (pre && live && v.s.step + 1 == p.L) {
-            const uint4* rp = p.rec + env * (RO_REC_BYTES / 16);
-#pragma unroll
-            for (int j = 0; j < 10; ++j) q[j] = rp[j];
-        }
         if (act_out && live) act_out[k * p.B + env] = pr.a;
         v.s.step = v.s.step < 0xFFFF ? v.s.step + 1 : 0xFFFF;
         const bool done = live && v.s.step == p.L;  // (:472)
@@ -882,6 +877,10 @@ __global__ __launch_bounds__(NB) void k_rollout_tpe(Params p, int K, int32_t* ac
                 wave_lds_sync();
             }
             if (do_reset) {
+                uint4 q[10];  // the next episode's record
+                const uint4* rp = p.rec + env * (RO_REC_BYTES / 16);
+#pragma unroll
+                for (int j = 0; j < 10; ++j) q[j] = rp[j];
                 tpe_start_episode(p, q, v, lat0, em, ed, olat, ocpu);
                 new_episode = true;
             }
