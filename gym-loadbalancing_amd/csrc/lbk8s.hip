@@ -131,8 +131,9 @@ __global__ void k_init(Params p, int trace) {
     for (int w = 0; w < p.NZW; ++w) p.nzone[w * p.B + env] = 0;
     p.acc2[env] = 0;
     p.acc3[env] = 0;
-    p.sum_lat[env] = 0.0;
-    p.sum_cpu[env] = 0.0;
+    p.sum_lat[env] = 0;
+    p.sum_cpu[env] = 0;
+    p.sum_hi[env] = 0;
     p.total[env] = 0.0;
     p.last_r[env] = p.init_last_r;
 }
@@ -198,7 +199,7 @@ __global__ void k_stats(Params p, double* out) {
     int64_t env = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (env >= p.B) return;
     write_stats_row(p, out + env * LB_ST_K, sc_unpack(p.sc[env]), p.acc2[env], p.acc3[env], p.total[env],
-                    p.sum_lat[env], p.sum_cpu[env]);
+                    p.sum_lat[env], p.sum_cpu[env], p.sum_hi[env]);
 }
 
 __global__ void k_status(Params p, uint32_t* flags) {
@@ -270,7 +271,7 @@ uint64_t align_up(uint64_t x) { return (x + 255) & ~(uint64_t)255; }
 
 struct Offsets {
     uint64_t lat_lut, cpu_lut, lat0, emeta, edyn, t, sc, topo, zcap, nzone, acc2, acc3, sum_lat,
-        sum_cpu, total, last_r, rec, end;
+        sum_cpu, sum_hi, total, last_r, rec, end;
 };
 
 Offsets offsets(const lb_config* c, int64_t B) {
@@ -293,6 +294,7 @@ Offsets offsets(const lb_config* c, int64_t B) {
     o.acc3 = take(B * 8);
     o.sum_lat = take(B * 8);
     o.sum_cpu = take(B * 8);
+    o.sum_hi = take(B * 4);
     o.total = take(B * 8);
     o.last_r = take(B * 8);
     // thread-per-env layout: k_rollout_tpe's next-episode records (scratch, per launch)
@@ -354,8 +356,9 @@ Params make_params(void* state, const lb_config* c, int64_t B) {
     p.nzone = (uint64_t*)(base + o.nzone);
     p.acc2 = (uint64_t*)(base + o.acc2);
     p.acc3 = (uint64_t*)(base + o.acc3);
-    p.sum_lat = (double*)(base + o.sum_lat);
-    p.sum_cpu = (double*)(base + o.sum_cpu);
+    p.sum_lat = (uint64_t*)(base + o.sum_lat);
+    p.sum_cpu = (uint64_t*)(base + o.sum_cpu);
+    p.sum_hi = (uint32_t*)(base + o.sum_hi);
     p.total = (double*)(base + o.total);
     p.last_r = (double*)(base + o.last_r);
     p.rec = g.tpe ? (uint4*)(base + o.rec) : nullptr;

@@ -179,8 +179,9 @@ struct Params {
     uint64_t* nzone;   // [NZW][B]  (word w of env at w*B + env)
     uint64_t* acc2;    // [B]
     uint64_t* acc3;    // [B]
-    double* sum_lat;   // [B]
-    double* sum_cpu;   // [B]
+    uint64_t* sum_lat; // [B] exact fixed-point sums (fix52, low 64 bits)
+    uint64_t* sum_cpu; // [B]
+    uint32_t* sum_hi;  // [B] their carries and the updated-topology residual D (xsum_add)
     double* total;     // [B]
     double* last_r;    // [B]
     uint4* rec;        // [B][RO_REC_BYTES / 16] next-episode records (thread-per-env rollout scratch)
@@ -274,26 +275,75 @@ __device__ __forceinline__ double accept_reward(const Params& p, double sel_lat,
     }
 }
 
+// ---- exact episode sums -------------------------------------------------------------
+// The reference's per-episode means are statistics.mean over lists of float64 values
+// (loadbalancer_k8s_env.py:451-454, :491-506): an exact rational sum, correctly rounded
+// once.  Every listed value (endpoint latency in [1, 500], endpoint cpu in [1, 100], an
+// updated topology latency fl(t * 1.7) in [1.7, 848.3]) is a float64 in [1, 1024), hence a
+// multiple of 2^-52 below 2^62 * 2^-52: it is accumulated EXACTLY as a fixed-point integer
+// fix52(x) = x * 2^52.  Episodes hold at most 1023 accepts (the history counters' range), so
+//   latency: lo u64 + 7 carry bits   (sum < 1023 * 500 * 2^52 < 2^71)
+//   cpu:     lo u64 + 5 carry bits   (sum < 1023 * 100 * 2^52 < 2^69)
+// and the updated topology sum needs no 64-bit word at all: with M = fix52(1.7) each term
+// is t * M - d(t), d(t) = t * M - fix52(fl(t * 1.7)) in [-202, 246] for t in [1, 499], so
+// the sum is intra * 2^52 + M * (sum_topo - intra) - D with D = sum of d, |D| < 2^18.
+// The carry word packs  lat carries [0,7) | cpu carries [7,12) | D (two's complement) [12,32).
+constexpr uint64_t FIX_17 = 7656119366529843ull;  // fix52(1.7) = fl(1.7) * 2^52
+constexpr int XH_CPU = 7, XH_D = 12;
+
+__device__ __forceinline__ uint64_t fix52(double x) {  // x in [1, 1024): x * 2^52, exactly
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    const int e = (int)(b >> 52) - 1023;
+    return ((b & 0x000fffffffffffffull) | 0x0010000000000000ull) << e;
+}
+// one accepted request's appends (:626-632): latency and cpu of the selected endpoint; an
+// inter-zone request's updated topology latency fl(tl * 1.7) adds its residual d(tl) to D
+__device__ __forceinline__ void xsum_add(uint64_t& lat, uint64_t& cpu, uint32_t& hi, double sel_lat,
+                                         double sel_cpu, int tl, bool inter) {
+    const uint64_t fl = fix52(sel_lat), fc = fix52(sel_cpu);
+    lat += fl;
+    cpu += fc;
+    uint32_t h = hi + (lat < fl ? 1u : 0u) + (cpu < fc ? (1u << XH_CPU) : 0u);
+    if (inter) h += (uint32_t)((uint64_t)tl * FIX_17 - fix52((double)tl * 1.7)) << XH_D;
+    hi = h;
+}
+// the exact sum (carries * 2^64 + lo) * 2^-52 as an unevaluated pair: s = the correctly
+// rounded float64 sum, r = the exact remainder (sum = s + r as rationals)
+__device__ __forceinline__ void xsum_pair(uint64_t lo, uint32_t carries, double& s, double& r) {
+    const double xh = (double)carries * 0x1p64 + (double)(uint32_t)(lo >> 32) * 0x1p32;
+    const double xl = (double)(uint32_t)lo;  // xh: <= 39 significant bits, exact
+    const double sum = xh + xl;              // one rounding
+    const double rem = xl - (sum - xh);      // Fast2Sum: xh is 0 or a multiple of 2^32 > xl
+    s = sum * 0x1p-52;  // exact scaling
+    r = rem * 0x1p-52;
+}
+
 // ep_stats row (include/lbk8s.h LB_ST_*) from the accumulators
 __device__ __forceinline__ void write_stats_row(const Params& p, double* out, const Scal& s, uint64_t acc2,
-                                                uint64_t acc3, double total, double sum_lat,
-                                                double sum_cpu) {
+                                                uint64_t acc3, double total, uint64_t sum_lat,
+                                                uint64_t sum_cpu, uint32_t sum_hi) {
     uint32_t sum_topo = (uint32_t)acc2;
+    double ls, lr, cs, cr;
+    xsum_pair(sum_lat, sum_hi & 0x7Fu, ls, lr);
+    xsum_pair(sum_cpu, (sum_hi >> XH_CPU) & 0x1Fu, cs, cr);
     out[LB_ST_RETURN] = total;
     out[LB_ST_LENGTH] = (double)s.step;
     out[LB_ST_ACCEPTED] = (double)s.acc;
-    out[LB_ST_SUM_LATENCY] = sum_lat;
+    out[LB_ST_SUM_LATENCY] = ls;
     out[LB_ST_SUM_TOPOLOGY] = (double)sum_topo;
     // intra-zone accepts see topology 1 (updated 1); inter ones topology * 1.7 (:582-593)
+    // (float64 approximation; the exact sum comes with LB_ST_SUM_TOPOLOGY_UPDATED_D)
     out[LB_ST_SUM_TOPOLOGY_UPDATED] = (double)s.intra + 1.7 * (double)(sum_topo - (uint32_t)s.intra);
     out[LB_ST_SUM_COST] = (double)(uint32_t)acc3;
-    out[LB_ST_SUM_CPU] = sum_cpu;
+    out[LB_ST_SUM_CPU] = cs;
     out[LB_ST_INTRA] = (double)s.intra;
     out[LB_ST_INTER] = (double)(s.acc - s.intra);
     out[LB_ST_GINI] = gini_of(acc2, s.acc, p.E);
     out[LB_ST_EPISODE] = (double)(uint32_t)(acc3 >> 32);
-#pragma unroll
-    for (int k = LB_ST_EPISODE + 1; k < LB_ST_K; ++k) out[k] = 0.0;
+    out[LB_ST_SUM_LATENCY_REM] = lr;
+    out[LB_ST_SUM_CPU_REM] = cr;
+    out[LB_ST_SUM_TOPOLOGY_UPDATED_D] = (double)((int32_t)sum_hi >> XH_D);
+    out[LB_ST_K - 1] = 0.0;
 }
 
 }  // namespace lbk

@@ -79,7 +79,9 @@ struct SEnv {
     double lat0[EPL];
     uint32_t em[EPL], ed[EPL];
     float olat[EPL], ocpu[EPL];  // observed endpoint latency / cpu (float32 obs columns 4, 2)
-    double t, dt, sum_lat, sum_cpu, total, last_r;
+    double t, dt, total, last_r;
+    uint64_t sum_lat, sum_cpu;  // exact fixed-point episode sums (xsum_add)
+    uint32_t sum_hi;
     uint64_t topo, zcap, acc2, acc3;
     uint64_t nz0, nz1;  // node-zone words 0 and 1 (nodes < 64), prefetched with the state
     Scal s;
@@ -174,6 +176,7 @@ __device__ __forceinline__ void slice_load(const Params& p, int64_t env, int lan
     v.nz1 = p.NZW > 1 ? p.nzone[p.B + env] : 0;
     v.sum_lat = p.sum_lat[env];
     v.sum_cpu = p.sum_cpu[env];
+    v.sum_hi = p.sum_hi[env];
     v.total = p.total[env];
     v.last_r = p.reward_fn != LB_REWARD_NAIVE ? p.last_r[env] : 0.0;
 }
@@ -186,6 +189,7 @@ __device__ __forceinline__ void slice_store_scalars(const Params& p, int64_t env
     p.acc3[env] = v.acc3;
     p.sum_lat[env] = v.sum_lat;
     p.sum_cpu[env] = v.sum_cpu;
+    p.sum_hi[env] = v.sum_hi;
     p.total[env] = v.total;
     if (p.reward_fn != LB_REWARD_NAIVE) p.last_r[env] = v.last_r;
 }
@@ -297,8 +301,9 @@ __device__ __forceinline__ void slice_reset(const Params& p, int64_t env, int la
     v.zcap = zc;
     v.acc2 = 0;
     v.acc3 = (uint64_t)episode << 32;
-    v.sum_lat = 0.0;
-    v.sum_cpu = 0.0;
+    v.sum_lat = 0;
+    v.sum_cpu = 0;
+    v.sum_hi = 0;
     v.total = 0.0;
     v.last_r = p.init_last_r;
     v.s.step = 0; v.s.acc = 0; v.s.intra = 0; v.s.penalty = 0; v.s.reset_done = 1;
@@ -389,8 +394,7 @@ __device__ __forceinline__ void slice_step_body(const Params& p, int64_t env, in
         v.acc3 += (uint64_t)node_cost(em_type(emA));
         v.s.acc = v.s.acc < 0xFFFF ? v.s.acc + 1 : 0xFFFF;
         if (v.s.rz == zA) v.s.intra = v.s.intra < 0xFFFF ? v.s.intra + 1 : 0xFFFF;
-        v.sum_lat += sel_lat;
-        v.sum_cpu += sel_cpu;
+        xsum_add(v.sum_lat, v.sum_cpu, v.sum_hi, sel_lat, sel_cpu, tl, v.s.rz != zA);
         // increase_resources / increase_endpoint_latency (:674-677) and the same step's
         // decrease in next_request() (:1137-1143) -> the history counters advance
 #pragma unroll
@@ -426,7 +430,7 @@ __device__ __forceinline__ void slice_step_body(const Params& p, int64_t env, in
     if (done && p.auto_reset) {
         if (p.term_obs) slice_write_obs<W, EPL>(p, p.term_obs, env, lane, v);
         if (p.ep_stats && lane == 0)
-            write_stats_row(p, p.ep_stats + env * LB_ST_K, v.s, v.acc2, v.acc3, v.total, v.sum_lat, v.sum_cpu);
+            write_stats_row(p, p.ep_stats + env * LB_ST_K, v.s, v.acc2, v.acc3, v.total, v.sum_lat, v.sum_cpu, v.sum_hi);
         slice_reset<W, EPL, TRACE>(p, env, lane, v);
     } else if (STORE_ED && accept) {
 #pragma unroll

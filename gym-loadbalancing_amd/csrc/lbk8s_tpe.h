@@ -24,8 +24,10 @@ constexpr int TPE_CW = 4 + 3 * TPE_E + 1;  // 29: odd stride -> conflict-free pe
 constexpr int TPE_FLAG = 1 << 5;
 
 struct TEnv {
-    double t, dt, sum_lat, sum_cpu, total, last_r;
+    double t, dt, total, last_r;
+    uint64_t sum_lat, sum_cpu;  // exact fixed-point episode sums (xsum_add)
     uint64_t topo, zcap, acc2, acc3, nz0, nz1;
+    uint32_t sum_hi;
     Scal s;
 };
 
@@ -218,8 +220,9 @@ __device__ void tpe_reset(const Params& p, int64_t env, TEnv& v, uint32_t* me) {
     v.zcap = zc;
     v.acc2 = 0;
     v.acc3 = (uint64_t)episode << 32;
-    v.sum_lat = 0.0;
-    v.sum_cpu = 0.0;
+    v.sum_lat = 0;
+    v.sum_cpu = 0;
+    v.sum_hi = 0;
     v.total = 0.0;
     v.last_r = p.init_last_r;
     v.s.step = 0; v.s.acc = 0; v.s.intra = 0; v.s.penalty = 0; v.s.reset_done = 1;
@@ -240,6 +243,7 @@ __device__ __forceinline__ void tpe_store_scalars(const Params& p, int64_t env, 
     *(p.acc3 + env) = (v.acc3);
     *(p.sum_lat + env) = (v.sum_lat);
     *(p.sum_cpu + env) = (v.sum_cpu);
+    *(p.sum_hi + env) = (v.sum_hi);
     *(p.total + env) = (v.total);
     if (p.reward_fn != LB_REWARD_NAIVE) *(p.last_r + env) = (v.last_r);
 }
@@ -438,8 +442,7 @@ __device__ __forceinline__ double tpe_apply(const Params& p, const TPrep& pr, in
         v.acc3 += (uint64_t)node_cost(em_type(emA));
         v.s.acc = v.s.acc < 0xFFFF ? v.s.acc + 1 : 0xFFFF;
         if (v.s.rz == zA) v.s.intra = v.s.intra < 0xFFFF ? v.s.intra + 1 : 0xFFFF;
-        v.sum_lat += sel_lat;
-        v.sum_cpu += sel_cpu;
+        xsum_add(v.sum_lat, v.sum_cpu, v.sum_hi, sel_lat, sel_cpu, tl, v.s.rz != zA);
         // increase_resources / increase_endpoint_latency (:674-677) and the same step's
         // decrease in next_request() (:1137-1143) -> the history counters advance
         const uint32_t edA_new = ((oA == ai ? (uint32_t)Mn : (uint32_t)ed_M(edA)) << 20) |
@@ -558,6 +561,7 @@ __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
     }
     v.sum_lat = *(p.sum_lat + ev);
     v.sum_cpu = *(p.sum_cpu + ev);
+    v.sum_hi = *(p.sum_hi + ev);
     v.total = *(p.total + ev);
     v.last_r = p.reward_fn != LB_REWARD_NAIVE ? *(p.last_r + ev) : 0.0;
 
@@ -578,7 +582,7 @@ __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
     // ---- VecEnv auto-reset: terminal obs + episode stats, then reset() below
     const uint64_t m = __ballot(do_reset);
     if (do_reset && p.ep_stats)
-        write_stats_row(p, p.ep_stats + env * LB_ST_K, v.s, v.acc2, v.acc3, v.total, v.sum_lat, v.sum_cpu);
+        write_stats_row(p, p.ep_stats + env * LB_ST_K, v.s, v.acc2, v.acc3, v.total, v.sum_lat, v.sum_cpu, v.sum_hi);
     if (keep) tpe_store_scalars(p, env, v);
     // get_state() rows built once per env, staged half a wave at a time; the finished envs'
     // post-reset obs come from their reset()
@@ -761,8 +765,9 @@ __device__ __forceinline__ void tpe_start_episode(const Params& p, const uint4 (
     const uint32_t episode = (uint32_t)(v.acc3 >> 32) + 1;
     v.acc3 = (uint64_t)episode << 32;
     v.acc2 = 0;
-    v.sum_lat = 0.0;
-    v.sum_cpu = 0.0;
+    v.sum_lat = 0;
+    v.sum_cpu = 0;
+    v.sum_hi = 0;
     v.total = 0.0;
     v.last_r = p.init_last_r;
     v.s.step = 0; v.s.acc = 0; v.s.intra = 0; v.s.penalty = 0; v.s.reset_done = 1;
@@ -809,6 +814,7 @@ __global__ __launch_bounds__(NB) void k_rollout_tpe(Params p, int K, int32_t* ac
     v.nz1 = p.NZW > 1 ? p.nzone[p.B + ev] : 0;
     v.sum_lat = p.sum_lat[ev];
     v.sum_cpu = p.sum_cpu[ev];
+    v.sum_hi = p.sum_hi[ev];
     v.total = p.total[ev];
     v.last_r = p.reward_fn != LB_REWARD_NAIVE ? p.last_r[ev] : 0.0;
     float olat[TPE_E], ocpu[TPE_E];  // observed endpoint latency / cpu (obs columns 4, 2)
@@ -867,7 +873,7 @@ __global__ __launch_bounds__(NB) void k_rollout_tpe(Params p, int K, int32_t* ac
         }
         const uint64_t m = __ballot(do_reset);
         if (do_reset && p.ep_stats)
-            write_stats_row(p, p.ep_stats + env * LB_ST_K, v.s, v.acc2, v.acc3, v.total, v.sum_lat, v.sum_cpu);
+            write_stats_row(p, p.ep_stats + env * LB_ST_K, v.s, v.acc2, v.acc3, v.total, v.sum_lat, v.sum_cpu, v.sum_hi);
         float* obs_k = p.obs ? p.obs + k * obs_slot : nullptr;
         if constexpr (PRE) {
             if (p.term_obs && m) {  // the finishing envs' terminal rows first
@@ -974,8 +980,9 @@ __global__ __launch_bounds__(NB) void k_rollout_tpe(Params p, int K, int32_t* ac
                 v.acc3 = u64(34);
                 v.s = sc_unpack(u64(36));
                 v.acc2 = 0;
-                v.sum_lat = 0.0;
-                v.sum_cpu = 0.0;
+                v.sum_lat = 0;
+                v.sum_cpu = 0;
+                v.sum_hi = 0;
                 v.total = 0.0;
                 v.last_r = p.init_last_r;
                 new_episode = true;

@@ -2,15 +2,18 @@
 
 Reference: loadbalancer_k8s_env.py:439-470 (13-key info, every value
 float("{:.2f}")), :472-510 (episode end, two save_to_csv rows) and
-utils.py:99-127 (CSV schema).  The GPU keeps exact integer counters and float64
-running sums per env; this module turns one env's accumulator row (the
-`ep_stats` layout below) into the reference's dict.
+utils.py:99-127 (CSV schema).  The GPU keeps exact integer counters and EXACT
+fixed-point sums of the float lists per env (lbk8s_common.h xsum_add); this module
+turns one env's accumulator row (the `ep_stats` layout below) into the reference's dict.
 
-Means: the reference uses statistics.mean (exact rational) over per-episode
-lists; here sum/count in float64.  For integer-valued lists (topology latency,
-cost) that is bit-identical; for float lists the 2-decimal value differs only
-when the exact mean lies within ~1e-13 of a rounding boundary.
+Means: the reference uses statistics.mean, i.e. the exact rational sum of the list
+divided by its length, rounded once to float64 (:451-454, :491-506).  The row carries
+each float sum exactly (a rounded float64 plus its exact remainder, or for the updated
+topology list an integer residual D, include/lbk8s.h), so the mean here is the same
+correctly rounded quotient, and "{:.2f}" formats the same float64.
 """
+from fractions import Fraction
+
 import numpy as np
 
 INFO_KEYS = ("reward_step", "action", "reward", "ep_block_prob", "ep_accepted_requests",
@@ -24,8 +27,10 @@ CSV_FIELDS = ("episode", "reward", "ep_block_prob", "ep_accepted_requests", "avg
 
 # ep_stats row layout (float64 x 16), shared with the C-ABI (include/lbk8s.h LB_ST_*)
 ST_RETURN, ST_LENGTH, ST_ACC, ST_SUM_LAT, ST_SUM_TOPO, ST_SUM_TOPO_UPD, ST_SUM_COST, \
-    ST_SUM_CPU, ST_INTRA, ST_INTER, ST_GINI, ST_EPISODE = range(12)
+    ST_SUM_CPU, ST_INTRA, ST_INTER, ST_GINI, ST_EPISODE, ST_SUM_LAT_REM, ST_SUM_CPU_REM, \
+    ST_SUM_TOPO_UPD_D = range(15)
 ST_K = 16
+FIX_17 = 7656119366529843  # fl(1.7) * 2^52: INCREASE_COST_PERCENTAGE (:67) at scale 2^-52
 
 
 def r2(x):
@@ -33,12 +38,22 @@ def r2(x):
     return float("{:.2f}".format(x))
 
 
+def exact_sums(st):
+    """The exact sums (Fractions) of the episode's latency, topology, cost, cpu and updated
+    topology lists from one ep_stats row."""
+    intra, topo = int(st[ST_INTRA]), int(st[ST_SUM_TOPO])
+    lat = Fraction(float(st[ST_SUM_LAT])) + Fraction(float(st[ST_SUM_LAT_REM]))
+    cpu = Fraction(float(st[ST_SUM_CPU])) + Fraction(float(st[ST_SUM_CPU_REM]))
+    upd = intra + Fraction(FIX_17 * (topo - intra) - int(st[ST_SUM_TOPO_UPD_D]), 1 << 52)
+    return lat, Fraction(topo), Fraction(int(st[ST_SUM_COST])), cpu, upd
+
+
 def _avgs(st):
-    acc = st[ST_ACC]
+    """statistics.mean of the five lists: float(exact sum / count), correctly rounded."""
+    acc = int(st[ST_ACC])
     if acc == 0:  # all four lists empty -> 1 (:444-449)
         return 1.0, 1.0, 1.0, 1.0, 1.0
-    return (st[ST_SUM_LAT] / acc, st[ST_SUM_TOPO] / acc, st[ST_SUM_COST] / acc,
-            st[ST_SUM_CPU] / acc, st[ST_SUM_TOPO_UPD] / acc)
+    return tuple(float(x / acc) for x in exact_sums(st))
 
 
 def step_info(st, reward, action, execution_time=0.0):
@@ -79,13 +94,11 @@ def csv_rows(st, episode, execution_time=0.0):
 
 
 def info_matrix(stats, rewards, actions):
-    """Vectorised 12 numeric info keys (no executionTime) for many envs: (B, 12) float64."""
+    """The 12 numeric info keys (no executionTime) for many envs: (B, 12) float64, each value
+    exactly the reference's float("{:.2f}") (step_info per row)."""
     stats = np.asarray(stats, np.float64)
-    acc = stats[:, ST_ACC]
-    step = np.maximum(stats[:, ST_LENGTH], 1)
-    safe = np.where(acc > 0, acc, 1)
-    avg = lambda k: np.where(acc > 0, stats[:, k] / safe, 1.0)  # noqa: E731
-    cols = [rewards, actions, stats[:, ST_RETURN], 1 - acc / step, acc, avg(ST_SUM_LAT),
-            avg(ST_SUM_TOPO), avg(ST_SUM_COST), avg(ST_SUM_CPU), stats[:, ST_INTRA] / step,
-            stats[:, ST_INTER] / step, stats[:, ST_GINI]]
-    return np.round(np.stack([np.asarray(c, np.float64) for c in cols], axis=1), 2)
+    out = np.empty((stats.shape[0], 12), np.float64)
+    for b in range(stats.shape[0]):
+        info = step_info(stats[b], float(rewards[b]), int(actions[b]))
+        out[b] = [info[k] for k in INFO_KEYS[:12]]
+    return out

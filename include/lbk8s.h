@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LBK8S_ABI_VERSION 4
+#define LBK8S_ABI_VERSION 5
 
 /* reward_function names of loadbalancer_k8s_env.py:20-31 */
 enum { LB_REWARD_NAIVE = 0, LB_REWARD_LATENCY = 1, LB_REWARD_FAIRNESS = 2, LB_REWARD_MULTI = 3 };
@@ -58,20 +58,30 @@ enum {
     LB_FIELD_DT = 11,                       /* dt of the current request   [B]   */
     LB_FIELD_COUNT = 12
 };
-/* ep_stats row (double x LB_ST_K) written for every env whose episode ends in a step */
+/* ep_stats row (double x LB_ST_K) written for every env whose episode ends in a step.
+ * The float sums are EXACT (statistics.mean semantics, loadbalancer_k8s_env.py:451-454):
+ *   sum(avg_endpoint_latency)  = [SUM_LATENCY] + [SUM_LATENCY_REM]   (as rationals; the
+ *   sum(avg_cpu_...)           = [SUM_CPU] + [SUM_CPU_REM]            first term is the
+ *                                                                      correctly rounded sum)
+ *   sum(avg_topology_latency_updated) = INTRA + (M * (SUM_TOPOLOGY - INTRA) - [..._D]) / 2^52,
+ *       M = fl(1.7) * 2^52 = 7656119366529843 ([SUM_TOPOLOGY_UPDATED] is a float64 approximation).
+ * The mean of a list is then the correctly rounded quotient of the exact sum by ACCEPTED. */
 enum {
     LB_ST_RETURN = 0,       /* total_reward                                  */
     LB_ST_LENGTH = 1,       /* current_step                                  */
     LB_ST_ACCEPTED = 2,     /* ep_accepted_requests                          */
-    LB_ST_SUM_LATENCY = 3,  /* sum(avg_endpoint_latency list)                */
+    LB_ST_SUM_LATENCY = 3,  /* sum(avg_endpoint_latency list), rounded       */
     LB_ST_SUM_TOPOLOGY = 4, /* sum(avg_topology_latency list)                */
-    LB_ST_SUM_TOPOLOGY_UPDATED = 5, /* sum(avg_topology_latency_updated)     */
+    LB_ST_SUM_TOPOLOGY_UPDATED = 5, /* sum(avg_topology_latency_updated), approx. */
     LB_ST_SUM_COST = 6,     /* sum(avg_cost list)                            */
-    LB_ST_SUM_CPU = 7,      /* sum(avg_cpu_usage_percentage_endpoint_selected) */
+    LB_ST_SUM_CPU = 7,      /* sum(avg_cpu_usage_percentage_endpoint_selected), rounded */
     LB_ST_INTRA = 8,        /* intra_zone_requests                           */
     LB_ST_INTER = 9,        /* inter_zone_requests                           */
     LB_ST_GINI = 10,        /* calculate_gini_coefficient(avg_load_served)   */
     LB_ST_EPISODE = 11,     /* episode index of this env (1-based)           */
+    LB_ST_SUM_LATENCY_REM = 12,        /* exact sum - [SUM_LATENCY]          */
+    LB_ST_SUM_CPU_REM = 13,            /* exact sum - [SUM_CPU]              */
+    LB_ST_SUM_TOPOLOGY_UPDATED_D = 14, /* integer D of the exact updated sum */
     LB_ST_K = 16
 };
 /* lb_config.geometry: which kernel shape (and so which state layout) serves E <= 8.

@@ -76,7 +76,7 @@ typedef struct {
     double *topo;     /* [B*Z*Z] */
     /* per-env scalars [B] */
     double *t, *dt, *sel_lat, *sel_topo, *sel_cpu, *total_reward;
-    double *sum_lat, *sum_topo_upd, *sum_cpu;
+    unsigned __int128 *sum_lat, *sum_topo_upd, *sum_cpu;  /* exact sums of the lists, x 2^52 */
     int64_t *sum_topo, *sum_cost;
     int32_t *step, *acc, *intra, *inter, *penalty, *pending, *req_zone, *req_thr, *req_node;
     uint32_t *episode;
@@ -143,6 +143,23 @@ static double fd_log(double x) {
     return dk * ln2_hi - ((hfsq - (sv * (hfsq + Rr) + dk * ln2_lo)) - f);
 }
 static double std_exp(uint32_t hi, uint32_t lo) { return -fd_log(1.0 - u53(hi, lo)); }
+
+/* ---------------- exact list sums (statistics.mean, :451-454) ------------- */
+/* Every value appended to the reference's float lists is a float64 in [1, 1024), so
+ * x * 2^52 is an integer below 2^62 and the list's exact sum is an integer at scale 2^-52
+ * (unsigned __int128 here).  The device keeps the same sums as 64-bit words plus packed
+ * carries (lbk8s_common.h xsum_add); both hand out the same ep_stats columns. */
+static unsigned __int128 fix52(double x) { return (unsigned __int128)(uint64_t)ldexp(x, 52); }
+/* the correctly rounded sum and its exact remainder (LB_ST_SUM_* / LB_ST_SUM_*_REM) */
+static void fix_pair(unsigned __int128 v, double* s, double* r) {
+    uint64_t hi = (uint64_t)(v >> 64), lo = (uint64_t)v;
+    double xh = ldexp((double)hi, 64) + ldexp((double)(uint32_t)(lo >> 32), 32);
+    double xl = (double)(uint32_t)lo;
+    double sum = xh + xl;
+    *s = ldexp(sum, -52);
+    *r = ldexp(xl - (sum - xh), -52);
+}
+#define FIX_17 7656119366529843ULL  /* fl(1.7) * 2^52 */
 
 /* ---------------- lifecycle ---------------------------------------------- */
 #define ALLOC(p, n) ((p) = calloc((size_t)(n), sizeof(*(p))))
@@ -237,7 +254,7 @@ static void reset_one(orc_env* s, int64_t b, const orc_reset_trace* tr) {
     int E = s->E, Z = s->Z, N = s->N;
     s->step[b] = 0; s->total_reward[b] = 0.0; s->acc[b] = 0; s->penalty[b] = 0;
     s->intra[b] = 0; s->inter[b] = 0;
-    s->sum_lat[b] = 0.0; s->sum_topo_upd[b] = 0.0; s->sum_cpu[b] = 0.0;
+    s->sum_lat[b] = 0; s->sum_topo_upd[b] = 0; s->sum_cpu[b] = 0;
     s->sum_topo[b] = 0; s->sum_cost[b] = 0;
     s->sel_lat[b] = 0.0; s->sel_topo[b] = 0.0; s->sel_cpu[b] = 1.0;   /* :325-327 */
     s->episode[b] += 1;
@@ -374,22 +391,28 @@ static double reward_of(const orc_env* s, int64_t b) {
 }
 
 enum { ST_RETURN, ST_LENGTH, ST_ACC, ST_SUM_LAT, ST_SUM_TOPO, ST_SUM_TOPO_UPD, ST_SUM_COST,
-       ST_SUM_CPU, ST_INTRA, ST_INTER, ST_GINI, ST_EPISODE, ST_K = 16 };
+       ST_SUM_CPU, ST_INTRA, ST_INTER, ST_GINI, ST_EPISODE, ST_SUM_LAT_REM, ST_SUM_CPU_REM,
+       ST_SUM_TOPO_UPD_D, ST_K = 16 };
 
 static void stats_of(const orc_env* s, int64_t b, double* st) {
     st[ST_RETURN] = s->total_reward[b];
     st[ST_LENGTH] = s->step[b];
     st[ST_ACC] = s->acc[b];
-    st[ST_SUM_LAT] = s->sum_lat[b];
+    fix_pair(s->sum_lat[b], &st[ST_SUM_LAT], &st[ST_SUM_LAT_REM]);
     st[ST_SUM_TOPO] = (double)s->sum_topo[b];
-    st[ST_SUM_TOPO_UPD] = s->sum_topo_upd[b];
+    /* float64 approximation (as the device writes it); the exact sum via D below */
+    st[ST_SUM_TOPO_UPD] = (double)s->intra[b] + 1.7 * (double)(s->sum_topo[b] - s->intra[b]);
     st[ST_SUM_COST] = (double)s->sum_cost[b];
-    st[ST_SUM_CPU] = s->sum_cpu[b];
+    fix_pair(s->sum_cpu[b], &st[ST_SUM_CPU], &st[ST_SUM_CPU_REM]);
     st[ST_INTRA] = s->intra[b];
     st[ST_INTER] = s->inter[b];
     st[ST_GINI] = gini(s, b);
     st[ST_EPISODE] = s->episode[b];
-    for (int k = ST_EPISODE + 1; k < ST_K; ++k) st[k] = 0.0;
+    /* D = intra * 2^52 + M * (sum_topo - intra) - exact updated sum (include/lbk8s.h) */
+    unsigned __int128 m = (unsigned __int128)s->intra[b] << 52;
+    m += (unsigned __int128)FIX_17 * (uint64_t)(s->sum_topo[b] - s->intra[b]);
+    st[ST_SUM_TOPO_UPD_D] = (double)(__int128)(m - s->sum_topo_upd[b]);
+    st[ST_K - 1] = 0.0;
 }
 
 /* step() :403-513 (+ VecEnv auto-reset when cfg.auto_reset) */
@@ -418,11 +441,11 @@ void orc_step(void* h, const int32_t* actions, float* obs, float* reward, uint8_
             double tu = in_zone == out_zone ? 1.0 : s->topo[(b * Z + in_zone) * Z + out_zone] *
                                                        INCREASE_COST_PERCENTAGE;
             s->sum_topo[b] += (int64_t)tl;
-            s->sum_topo_upd[b] += tu;
-            s->sum_lat[b] += s->ep_lat[i];
+            s->sum_topo_upd[b] += fix52(tu);
+            s->sum_lat[b] += fix52(s->ep_lat[i]);
             s->sum_cost[b] += cost;
             s->loads[i] += 1.0;
-            s->sum_cpu[b] += s->ep_cpu[i];
+            s->sum_cpu[b] += fix52(s->ep_cpu[i]);
             s->sel_lat[b] = s->ep_lat[i];
             s->sel_topo[b] = tl;
             s->sel_cpu[b] = s->ep_cpu[i];

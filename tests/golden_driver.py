@@ -78,7 +78,7 @@ def replay(d, backend, check_state=True, n_steps=None, policy=None):
         else:
             _eq("obs", obs, exp_obs, where)
             stats = backend.stats()
-        # info: integer-valued keys must be exact; float means within one 2-dp unit
+        # info: every key exactly the reference's float("{:.2f}") (exact-rational means)
         info = d["info"][:, s]
         for b in range(B):
             got = step_info(stats[b], float(d["reward"][b, s]), int(actions[b]))
@@ -88,12 +88,9 @@ def replay(d, backend, check_state=True, n_steps=None, policy=None):
                              "ep_inter_zone_percentage", "gini"], info[b, :12]))
             for key, ev in expv.items():
                 counts["info_total"] += 1
-                if got[key] == ev:
-                    counts["info_exact"] += 1
-                elif key in ("avg_endpoint_latency", "avg_cpu_endpoint_selected", "reward"):
-                    assert abs(got[key] - ev) <= 0.0100001, (key, got[key], ev, where, b)
-                else:
+                if got[key] != ev:
                     raise AssertionError(f"info[{key}] {got[key]} != {ev} at {where} env {b}")
+                counts["info_exact"] += 1
             assert int(stats[b, ST_ACC]) == d["state_counters"][b, s, 1]
             assert int(stats[b, ST_INTRA]) == d["state_counters"][b, s, 2]
             assert int(stats[b, ST_INTER]) == d["state_counters"][b, s, 3]

@@ -47,8 +47,7 @@ def test_oracle_matches_reference(oracle_mod, name):
         policy = lambda b: b.o.policy_greedy(kind)  # noqa: E731
     c = replay(d, be, policy=policy)
     assert c["steps"] == d["actions"].shape[1]
-    # float means may differ from statistics.mean's exact rational only at rounding ties
-    assert c["info_exact"] >= 0.999 * c["info_total"]
+    assert c["info_exact"] == c["info_total"]
 
 
 def test_oracle_csv_rows_match_reference(oracle_mod):
@@ -69,8 +68,8 @@ def test_oracle_csv_rows_match_reference(oracle_mod):
                 exp_r, exp_u = d["csv_results"][b, ep], d["csv_no_cost_updated"][b, ep]
                 got_r = np.array(list(res.values())[:-1])
                 got_u = np.array(list(upd.values())[:-1])
-                np.testing.assert_allclose(got_r, exp_r[:-1], atol=0.0100001, rtol=0)
-                np.testing.assert_allclose(got_u, exp_u[:-1], atol=0.0100001, rtol=0)
+                np.testing.assert_array_equal(got_r, exp_r[:-1])
+                np.testing.assert_array_equal(got_u, exp_u[:-1])
             k += 1
             ep += 1
     assert ep == d["csv_results"].shape[1]
