@@ -204,12 +204,17 @@ def main(argv=None):
     def one_step(i):  # actions=None: the env's random policy, drawn inside the step kernel
         env.step_device(None, obs_out=obs_ring[i % T], reward_out=rew_ring[i % T], done_out=done_ring[i % T])
 
-    def one_launch(mode, i, end):  # -> vector steps launched from step i
+    launched = []  # vector steps per launch issued by run() (graph replays count their launches)
+
+    def one_launch(mode, i, end, record=True):  # -> vector steps launched from step i
         if mode == "step":
             one_step(i)
-            return 1
-        n = min(T - i % T, end - i)  # K = the ring's remaining slots: T steps per launch
-        env.rollout("random", n, obs_out=obs_ring[i % T], reward_out=rew_ring[i % T], done_out=done_ring[i % T])
+            n = 1
+        else:
+            n = min(T - i % T, end - i)  # K = the ring's remaining slots: T steps per launch
+            env.rollout("random", n, obs_out=obs_ring[i % T], reward_out=rew_ring[i % T], done_out=done_ring[i % T])
+        if record:
+            launched.append(n)
         return n
 
     # setup: stagger the episodes so 1/L of the envs end (and auto-reset) at every step
@@ -229,22 +234,27 @@ def main(argv=None):
                 one_step(0)
             stream.wait_stream(side)
             graph = torch.cuda.CUDAGraph()
+            graph_launches = []
             with torch.cuda.graph(graph):
                 i = 0
                 while i < T:
-                    i += one_launch(mode, i, T)
+                    n = one_launch(mode, i, T, record=False)
+                    graph_launches.append(n)
+                    i += n
 
         def run(first, count):
             i, end = first, first + count
             while i < end:
                 if graph is not None and i % T == 0 and end - i >= T:
                     graph.replay()
+                    launched.extend(graph_launches)
                     i += T
                 else:
                     i += one_launch(mode, i, end)
 
         run(0, args.warmup)
         K = args.steps
+        del launched[:]
         ep0 = env.stats()[:, ST_EPISODE].sum().item()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         # timed: exactly K steps, barrier + synchronize on both sides; HIP events on the
@@ -274,34 +284,45 @@ def main(argv=None):
             dist.all_reduce(v)
             resets = int(v[0].item())
         del graph
-        return dict(el=el, kernel_ms=kernel_ms, resets=resets, graphs=not args.no_graph)
+        return dict(el=el, kernel_ms=kernel_ms, resets=resets, graphs=not args.no_graph, launches=list(launched))
 
     K = args.steps
     res = measure(args.launch)
     step_res = measure("step") if args.launch == "rollout" and not args.no_step_line else None
     el, kernel_ms, resets = res["el"], res["kernel_ms"], res["resets"]
+    launches = res["launches"]
+    assert sum(launches) == K, (launches, K)
     value = total * K / el
     b_step = algorithmic_bytes(env.cfg, reads_actions=False)
     out_b = 32 * R + 5  # obs rows + reward + done, written every step
-    # a rollout launch reads and writes the state once for its T steps
-    b_alg = b_step if args.launch == "step" else out_b + (b_step - out_b) / T
+    # byte model: lb_step moves b_step per env-step; an lb_rollout launch of k steps
+    # writes out_b per env-step and reads + writes the state once: b_step - out_b per env per
+    # launch.  Priced on the launches the timed window actually issued.
+    n_launch = len(launches)
+    k_avg = K / n_launch
+    if args.launch == "step":
+        b_alg, model = b_step, f"lb_step: {b_step} B per env-step (SURVEY 8d: 53E + 6Z + 236)"
+    else:
+        b_alg = out_b + (b_step - out_b) * n_launch / K
+        model = f"lb_rollout: {out_b} + {b_step - out_b}/k B per env-step, k = {launches[0] if len(set(launches)) == 1 else launches} steps per launch"
     achieved = b_alg * B / (kernel_ms * 1e-3) / 1e9
     traffic = None
     pmc_path = args.pmc_json if args.launch == "step" else args.pmc_json.replace(".json", "_rollout.json")
     try:
         with open(pmc_path) as f:
             pmc = json.load(f)
-        if (pmc.get("config") == args.config and pmc.get("envs") == B
-                and pmc.get("steps_per_launch", 1) == (T if args.launch == "rollout" else 1)):
-            traffic = pmc.get("hbm_bytes_per_launch")  # per launch: T steps in rollout mode
+        # only a PMC pass of the same launch shape (config, envs, steps per launch) prices this line
+        if (pmc.get("config") == args.config and pmc.get("envs") == B and len(set(launches)) == 1
+                and pmc.get("steps_per_launch", 1) == launches[0]):
+            traffic = pmc.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
     tpe = env.cfg.num_endpoints <= 8 and (args.geometry == "tpe" or (args.geometry == "auto" and B >= 32768))
     if args.launch == "step":
         kname = "k_step_tpe (lb_step, auto-reset inside)" if tpe else "k_step_slice (lb_step)"
     else:
-        kname = (f"k_rollout_tpe (lb_rollout, {T} steps per launch, random policy, auto-reset inside)" if tpe
-                 else f"k_rollout_slice (lb_rollout, {T} steps per launch)")
+        kname = (f"k_rollout_lean (lb_rollout, random policy, auto-reset inside)" if tpe
+                 else f"k_rollout_slice (lb_rollout)")
     line = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": K,
         "warmup": args.warmup, "ms_per_step": el / K * 1e3, "higher_is_better": True,
@@ -311,26 +332,24 @@ def main(argv=None):
                                f"(E={env.cfg.num_endpoints}, N={env.cfg.num_nodes}, Z={env.cfg.num_zones}, "
                                f"{env.cfg.reward_function}), {B} per GPU, obs ring T={T}, "
                                + ("lockstep" if args.lockstep else "staggered") + " episodes, "
-                               + (f"{T} vector steps per lb_rollout launch" if args.launch == "rollout"
-                                  else "one lb_step launch per vector step"),
+                               + (f"timed as {n_launch} lb_rollout launch(es) of {launches} vector steps"
+                                  if args.launch == "rollout" else "one lb_step launch per vector step"),
                    "envs_per_gpu": B, "total_envs": total, "scenario": args.config, "episode_length": L,
                    "resets_in_window": resets, "graphs": res["graphs"], "geometry": args.geometry,
                    "launch": args.launch, "parallelism": f"env-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
-                     "kernel_ms": kernel_ms, "bytes_per_env_step": b_alg, "envs_per_launch": B,
-                     "steps_per_launch": T if args.launch == "rollout" else 1,
+                     "kernel_ms": kernel_ms, "bytes_per_env_step": b_alg, "byte_model": model,
+                     "envs_per_launch": B, "launches_timed": n_launch, "steps_per_launch": k_avg,
                      # one launch = steps_per_launch vector steps: the rocprof average duration
-                     # of the kernel is launch_ms; traffic is HBM bytes per launch (PMC)
-                     "launch_ms": kernel_ms * (T if args.launch == "rollout" else 1),
-                     "traffic_bytes_per_env_step": (traffic / B / (T if args.launch == "rollout" else 1)
-                                                    if traffic is not None else None),
+                     # of the kernel is launch_ms; traffic is HBM bytes per launch (PMC, same k)
+                     "launch_ms": kernel_ms * k_avg,
+                     "traffic_bytes_per_env_step": (traffic / B / k_avg if traffic is not None else None),
                      # the same time against SURVEY 8(d)'s per-env-step bytes of the one-launch-
                      # per-step design (the rollout moves fewer: frac > 1 there means it beats
                      # that design's bandwidth bound), and against the PMC-measured bytes
                      "frac_at_survey_bytes": b_step * B / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "frac_measured_traffic": (traffic / (T if args.launch == "rollout" else 1)
-                                               / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                     "frac_measured_traffic": (traffic / k_avg / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
                                                if traffic is not None else None)},
     }
     if step_res is not None:

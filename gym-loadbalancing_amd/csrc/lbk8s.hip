@@ -27,6 +27,7 @@
 #include "lbk8s_ds_train.h"
 #include "lbk8s_slice.h"
 #include "lbk8s_tpe.h"
+#include "lbk8s_rollout.h"
 
 namespace lbk {
 
@@ -78,6 +79,53 @@ __global__ void k_replay_add(ReplayParams p) {
         }
         if (i == 0) *p.pos_out = (pos + 1) % p.slots;
     }
+}
+
+// lb_episode_log: VecMonitor's per-env float32 return and the finished episodes' rows,
+// appended to a device log (one atomic per wave: the ballot's count)
+struct EpLogParams {
+    int64_t B;
+    const uint8_t* done;
+    const double* ep_stats;
+    const float* reward;
+    const int32_t* actions;
+    float* ret32;
+    float* ep_r32;
+    int64_t tag;
+    double* log;
+    int64_t cap;
+    uint32_t* count;
+};
+
+__global__ __launch_bounds__(256) void k_episode_log(EpLogParams p) {
+    const int64_t env = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const bool live = env < p.B;
+    bool d = false;
+    float r32 = 0.f;
+    if (live) {
+        r32 = p.ret32[env] + p.reward[env];  // float32, as VecMonitor's episode_returns
+        d = p.done[env] != 0;
+        p.ret32[env] = d ? 0.f : r32;
+        if (d && p.ep_r32) p.ep_r32[env] = r32;
+    }
+    const uint64_t m = __ballot(d);
+    if (!m) return;
+    uint32_t base = 0;
+    if (lane == __ffsll((unsigned long long)m) - 1) base = atomicAdd(p.count, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, __ffsll((unsigned long long)m) - 1);
+    if (!d) return;
+    const int64_t slot = (int64_t)base + __popcll(m & ((1ull << lane) - 1));
+    if (slot >= p.cap) return;
+    double* row = p.log + slot * LB_EPLOG_W;
+    const double* st = p.ep_stats + env * LB_ST_K;
+#pragma unroll
+    for (int k = 0; k < LB_ST_K; ++k) row[k] = st[k];
+    row[LB_EPLOG_RET32] = (double)r32;
+    row[LB_EPLOG_REWARD] = (double)p.reward[env];
+    row[LB_EPLOG_ACTION] = (double)p.actions[env];
+    row[LB_EPLOG_ENV] = (double)env;
+    row[LB_EPLOG_TAG] = (double)p.tag;
 }
 
 // LAT[k][j]: endpoint latency after j selections from trunc(initial) = k
@@ -215,6 +263,9 @@ __global__ void k_status(Params p, uint32_t* flags) {
 
 // ---- host side ---------------------------------------------------------------------------
 thread_local std::string g_err;
+// experiment switch (lbx_set_rollout_variant, tools/roll_variants.py): 3 = the round-2
+// k_rollout_tpe for the L >= K launches k_rollout_img serves (an A/B reference)
+int g_rollout_variant = 0;
 
 int fail(const char* msg) {
     g_err = msg;
@@ -435,6 +486,8 @@ extern "C" {
 
 int lb_abi_version(void) { return LBK8S_ABI_VERSION; }
 
+int lbx_set_rollout_variant(int v) { g_rollout_variant = v; return 0; }
+
 const char* lb_last_error(void) { return g_err.c_str(); }
 
 int lb_validate_config(const lb_config* cfg) { return validate(cfg); }
@@ -563,6 +616,22 @@ int lb_rollout(void* state, const lb_config* cfg, int64_t num_envs, int32_t poli
         // episodes at least as long as the launch (an env ends at most once in it): next
         // episodes drawn before the first step
         const bool pre = cfg->auto_reset && cfg->episode_length >= steps;
+        if (pre && g_rollout_variant != 3) {  // k_rollout_img (lbk8s_rollout.h)
+            const bool e8 = p.E == 8 && p.R == 9;
+#define LB_IMG(NB_, KIND_)                                                                                   \
+            if (e8) hipLaunchKernelGGL((k_rollout_img<NB_, KIND_, 8, 9, 4>), grid, block, 0, s, p, (int)steps, actions_out); \
+            else hipLaunchKernelGGL((k_rollout_img<NB_, KIND_, 0, 0, 4>), grid, block, 0, s, p, (int)steps, actions_out);
+#define LB_IMG_KIND(KIND_) if (small) { LB_IMG(64, KIND_) } else { LB_IMG(BLOCK, KIND_) }
+            switch (policy) {
+            case LB_POLICY_TOPOLOGY_GREEDY: LB_IMG_KIND(LB_POLICY_TOPOLOGY_GREEDY); break;
+            case LB_POLICY_ZONE_CPU_GREEDY: LB_IMG_KIND(LB_POLICY_ZONE_CPU_GREEDY); break;
+            case LB_POLICY_ENDPOINT_CPU_GREEDY: LB_IMG_KIND(LB_POLICY_ENDPOINT_CPU_GREEDY); break;
+            default: LB_IMG_KIND(LB_POLICY_RANDOM); break;
+            }
+#undef LB_IMG_KIND
+#undef LB_IMG
+            return check_launch();
+        }
 #define LB_ROLLOUT_TPE_NB(NB_, KIND_)                                                                         \
         if (pre) hipLaunchKernelGGL((k_rollout_tpe<NB_, KIND_, true>), grid, block, 0, s, p, (int)steps, actions_out); \
         else hipLaunchKernelGGL((k_rollout_tpe<NB_, KIND_, false>), grid, block, 0, s, p, (int)steps, actions_out);
@@ -645,6 +714,16 @@ int lb_status(const void* state, const lb_config* cfg, int64_t num_envs, uint32_
     hipStream_t s = (hipStream_t)stream;
     if (hipMemsetAsync(flags_out, 0, sizeof(uint32_t), s) != hipSuccess) return fail("hipMemsetAsync failed");
     hipLaunchKernelGGL(k_status, dim3(env_blocks(num_envs)), dim3(BLOCK), 0, s, p, flags_out);
+    return check_launch();
+}
+
+int lb_episode_log(int64_t num_envs, const uint8_t* done, const double* ep_stats, const float* reward,
+                   const int32_t* actions, float* ret32, float* ep_r32, int64_t tag, double* log, int64_t cap,
+                   uint32_t* count, void* stream) {
+    if (num_envs < 1 || !done || !ep_stats || !reward || !actions || !ret32 || !log || !count || cap < 0)
+        return fail("episode log: buffers NULL or num_envs < 1");
+    EpLogParams p{num_envs, done, ep_stats, reward, actions, ret32, ep_r32, tag, log, cap, count};
+    hipLaunchKernelGGL(k_episode_log, dim3(env_blocks(num_envs)), dim3(BLOCK), 0, (hipStream_t)stream, p);
     return check_launch();
 }
 

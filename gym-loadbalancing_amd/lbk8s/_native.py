@@ -21,6 +21,8 @@ LB_FIELD = {"endpoint_latency": 0, "endpoint_cpu_usage_percentage": 1,
             "request_zone": 9, "request_threshold": 10}
 PER_ENV_FIELDS = {"current_time", "current_step", "request_zone", "request_threshold"}
 LB_ST_K = 16
+LB_EPLOG_W = 24
+LB_EPLOG_RET32, LB_EPLOG_REWARD, LB_EPLOG_ACTION, LB_EPLOG_ENV, LB_EPLOG_TAG = 16, 17, 18, 19, 20
 LB_STATUS_BAD_ACTION, LB_STATUS_NOT_RESET = 1, 2
 LB_GEOMETRY = {"auto": 0, "tpe": 1, "slice": 2}
 
@@ -105,10 +107,11 @@ def lib():
     L.lb_ds_train_forward.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp, vp]
     L.lb_ds_pack_backward.argtypes = [C.POINTER(LBDSWeightsC), vp, vp]
     L.lb_ds_train_backward.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.lb_episode_log.argtypes = [i64, vp, vp, vp, vp, vp, vp, i64, vp, i64, vp, vp]
     for f in ("lb_validate_config", "lb_state_bytes", "lb_init", "lb_reset", "lb_step", "lb_policy", "lb_rollout",
               "lb_get_field", "lb_get_stats", "lb_status", "lb_ds_pack", "lb_ds_forward",
               "lb_ds_train_forward", "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax",
-              "lb_replay_add", "lb_ppo_head"):
+              "lb_replay_add", "lb_ppo_head", "lb_episode_log"):
         getattr(L, f).restype = C.c_int
     v = L.lb_abi_version()
     if v != ABI_VERSION:
@@ -130,4 +133,5 @@ def check(rc):
 EXPORTED_SYMBOLS = ("lb_abi_version", "lb_last_error", "lb_validate_config", "lb_state_bytes",
                     "lb_init", "lb_reset", "lb_step", "lb_policy", "lb_rollout", "lb_get_field", "lb_get_stats",
                     "lb_status", "lb_ds_pack", "lb_ds_forward", "lb_ds_train_forward",
-                    "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax", "lb_replay_add", "lb_ppo_head")
+                    "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax", "lb_replay_add", "lb_ppo_head",
+                    "lb_episode_log")

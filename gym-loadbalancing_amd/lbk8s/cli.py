@@ -86,14 +86,17 @@ def get_env(env_name, rejection, num_endpoints, num_zones, num_nodes, reward_fun
                     **env_kwargs(rejection, num_endpoints, num_zones, num_nodes, reward_function))
 
 
-def get_model(alg, env):
-    """get_model (run.py:54-72) for the deep-sets algorithms."""
+def get_model(alg, env, rank=0):
+    """get_model (run.py:54-72) for the deep-sets algorithms.  With several ranks each rank's
+    learner seed is offset by its rank, so rollout uniforms, minibatch permutations, replay
+    samples and exploration coins differ across GPUs (the parameters are broadcast from rank
+    0, so the replicas still start identical)."""
     if alg == "ppo_deepsets":
         from .ppo import PPO_DeepSets
-        return PPO_DeepSets(env, num_steps=100, n_minibatches=8, ent_coef=0.001, seed=2)
+        return PPO_DeepSets(env, num_steps=100, n_minibatches=8, ent_coef=0.001, seed=2 + rank)
     if alg == "dqn_deepsets":
         from .dqn import DQN_DeepSets
-        return DQN_DeepSets(env, num_steps=100, n_minibatches=8)
+        return DQN_DeepSets(env, num_steps=100, n_minibatches=8, seed=1 + rank)
     if alg in SB3_ALGS:
         raise SystemExit(f"{alg!r} is a stable-baselines3 model; this framework provides the deep-sets "
                          "algorithms (ppo_deepsets, dqn_deepsets) and LBVecEnv as a VecEnv")
@@ -128,7 +131,7 @@ def main(argv=None):
         env = get_env(args.env_name, args.rejection, num_endpoints, num_zones, num_nodes, reward,
                       num_envs=args.num_envs, device=dev if world > 1 else args.device, seed=args.seed,
                       env_id_offset=rank * args.num_envs, monitor_file=mon)
-        model = get_model(alg, env)
+        model = get_model(alg, env, rank)
         if args.loading:  # resume training
             model.load(args.load_path)
         model.learn(total_timesteps=total_steps)

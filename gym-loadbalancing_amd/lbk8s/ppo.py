@@ -300,8 +300,15 @@ class PPO_DeepSets:
                 else:
                     out = self._minibatch_step(*(t[mb] for t in src))
                 loss, pg, vl, ent, kl, cf = out
-            if self.target_kl is not None and kl > self.target_kl:
-                break
+            if self.target_kl is not None:
+                # every rank takes the same decision (one rank leaving the epoch loop early
+                # would skip collectives the others still issue): the mean kl over the ranks
+                kl_all = kl.detach().clone()
+                if self._multi:
+                    lbdist.all_reduce_sum(kl_all)
+                    kl_all /= torch.distributed.get_world_size()
+                if kl_all > self.target_kl:
+                    break
         if self.use_graphs:
             fused.invalidate(self.agent)  # replayed Adam steps do not move the version counters
         stats.update(loss=loss.item(), pg_loss=pg.item(), v_loss=vl.item(), entropy=ent.item(),

@@ -85,8 +85,8 @@ class LazyInfos:
         info = step_info(st, float(self._r[i]), int(self._a[i]))
         if self._d[i] and env.auto_reset:
             info["terminal_observation"] = env._host_terminal_obs()[i]
-            if env.monitor:
-                ep = {"r": float(st[ST_RETURN]), "l": int(st[ST_LENGTH]),
+            if env.monitor:  # (VecMonitor: the float32 running return)
+                ep = {"r": float(env._host_ep_r32()[i]), "l": int(st[ST_LENGTH]),
                       "t": round(time.time() - env._t_start, 6)}
                 for k in env.info_keywords:
                     ep[k] = info[k]
@@ -111,10 +111,14 @@ class _MonitorWriter:
         self.w.writerow(["r", "l", "t"] + list(self.keys))
         self.f.flush()
 
-    def write(self, rows, rewards, actions, t):
-        for st, r, a in zip(rows, rewards, actions):
-            info = step_info(st, float(r), int(a))
-            self.w.writerow([round(float(st[ST_RETURN]), 6), int(st[ST_LENGTH]), round(t - self.t_start, 6)]
+    def write(self, rows, t):
+        """rows: episode-log rows (lb_episode_log layout); t: host time of each row's step.
+        'r' is VecMonitor's float32 running return."""
+        for row, tt in zip(rows, t):
+            info = step_info(row[:_native.LB_ST_K], float(row[_native.LB_EPLOG_REWARD]),
+                             int(row[_native.LB_EPLOG_ACTION]))
+            r32 = np.float32(row[_native.LB_EPLOG_RET32])
+            self.w.writerow([round(r32, 6), int(row[ST_LENGTH]), round(tt - self.t_start, 6)]
                             + [info[k] for k in self.keys])
         self.f.flush()
 
@@ -170,7 +174,15 @@ class LBVecEnv:
         self._t_start = time.time()
         self._host_cache = {}
         self._monitor = _MonitorWriter(monitor_file, self._t_start, self.info_keywords) if monitor_file else None
-        self._mon_pending = []
+        if self.monitor:  # VecMonitor: float32 running returns and the device episode log
+            self._ret32 = torch.zeros(B, dtype=torch.float32, device=dev)
+            self._ep_r32 = torch.zeros(B, dtype=torch.float32, device=dev)
+            # an env finishes at most once per episode_length steps, so flushing every
+            # min(64, L) steps never holds more than B rows
+            self._log = torch.empty((B, _native.LB_EPLOG_W), dtype=torch.float64, device=dev)
+            self._log_count = torch.zeros(1, dtype=torch.int32, device=dev)
+            self._log_every = max(1, min(64, self.cfg.episode_length))
+            self._log_times = []
         if self.trace_mode:
             if t0 is None:
                 raise ValueError("trace mode needs t0 (current_time after __init__) per env")
@@ -220,6 +232,11 @@ class LBVecEnv:
         if "ep_stats" not in self._host_cache:
             self._host_cache["ep_stats"] = self.ep_stats.cpu().numpy()
         return self._host_cache["ep_stats"]
+
+    def _host_ep_r32(self):
+        if "r32" not in self._host_cache:
+            self._host_cache["r32"] = self._ep_r32.cpu().numpy()
+        return self._host_cache["r32"]
 
     def _host_terminal_obs(self):
         if "term" not in self._host_cache:
@@ -286,7 +303,7 @@ class LBVecEnv:
         infos = LazyInfos(self, self.rewards, self.actions, self.dones, self._t_start)
         if self.save_csv:
             self._write_csv()
-        if self._monitor is not None:
+        if self.monitor:
             self.record_episodes()
             self.flush_monitor()
         if self.as_tensors:
@@ -358,26 +375,39 @@ class LBVecEnv:
 
     # ---- VecMonitor file ------------------------------------------------------------------------
     def record_episodes(self, dones=None, rewards=None, actions=None):
-        """Queue the episodes finished by the last step for the monitor file (device copies;
-        the host reads them at flush_monitor).  The device learners call this after every
-        step_device with the buffers they passed it; the drop-in step() does it itself."""
-        if self._monitor is None:
+        """VecMonitor bookkeeping of the last vector step, on the device: the float32 running
+        returns and, for the finished envs only, their rows appended to the episode log
+        (lb_episode_log; nothing per env crosses to the host).  The device learners call this
+        after every step_device with the buffers they passed it; the drop-in step() does it
+        itself.  The host reads the log at flush_monitor (every min(64, L) steps)."""
+        if not self.monitor:
             return
         d = self.dones if dones is None else dones
         r = self.rewards if rewards is None else rewards
         a = self.actions if actions is None else actions
-        self._mon_pending.append((d.clone(), self.ep_stats[:, :12].clone(), r.clone(), a.clone(), time.time()))
-        if len(self._mon_pending) >= 64:
+        _native.check(self._L.lb_episode_log(
+            self.num_envs, self._ptr(d), self._ptr(self.ep_stats), self._ptr(r), self._ptr(a),
+            self._ptr(self._ret32), self._ptr(self._ep_r32), len(self._log_times), self._ptr(self._log),
+            self.num_envs, self._ptr(self._log_count), self._stream()))
+        self._log_times.append(time.time())
+        if len(self._log_times) >= self._log_every:
             self.flush_monitor()
 
     def flush_monitor(self):
-        if self._monitor is None or not self._mon_pending:
+        """Write the logged episodes (one host sync): in step order, env order within a step."""
+        if not self.monitor or not self._log_times:
             return
-        for d, st, r, a, t in self._mon_pending:
-            dn = d.cpu().numpy().astype(bool)
-            if dn.any():
-                self._monitor.write(st.cpu().numpy()[dn], r.cpu().numpy()[dn], a.cpu().numpy()[dn], t)
-        self._mon_pending = []
+        n = int(self._log_count.item())
+        if n > self.num_envs:
+            raise RuntimeError(f"episode log overflow ({n} rows > {self.num_envs})")
+        rows = self._log[:n].cpu().numpy() if n else np.zeros((0, _native.LB_EPLOG_W))
+        order = np.lexsort((rows[:, _native.LB_EPLOG_ENV], rows[:, _native.LB_EPLOG_TAG]))
+        rows = rows[order]
+        if self._monitor is not None and n:
+            t = [self._log_times[int(g)] for g in rows[:, _native.LB_EPLOG_TAG]]
+            self._monitor.write(rows, t)
+        self._log_count.zero_()
+        self._log_times = []
 
     def reset_masked(self, mask):
         """reset() of the envs where mask (B,) is nonzero; the others keep their episode."""

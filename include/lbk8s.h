@@ -252,6 +252,21 @@ int lb_replay_add(int64_t num_envs, int32_t obs_floats, int64_t slots, const int
                   int64_t* rb_actions, float* rb_rewards, float* rb_dones, double* ep_sum, double* ep_cnt,
                   void* stream);
 
+/* ---- Episode log (SB3 VecMonitor, run.py:122) -------------------------------------------
+ * After a vector step: every env's float32 running return ret32[b] += reward[b] (VecMonitor
+ * sums the float32 rewards, stable_baselines3 vec_monitor.py), and every env with done[b]
+ * appends one LB_EPLOG_W-double row to log [cap][LB_EPLOG_W] at an index taken from the
+ * device counter *count (rows past cap are dropped; *count still counts them), then its
+ * ret32 restarts at 0 (ep_r32[b] keeps the finished return; may be NULL).  Row: the env's
+ * ep_stats row (LB_ST_K doubles), then the float32 return, the step's reward, its action,
+ * the env index and `tag` (the caller's step counter; rows are unordered within a call).
+ * Only the finished envs' rows move: the log grows with episodes, not with num_envs. */
+#define LB_EPLOG_W 24
+enum { LB_EPLOG_RET32 = 16, LB_EPLOG_REWARD = 17, LB_EPLOG_ACTION = 18, LB_EPLOG_ENV = 19, LB_EPLOG_TAG = 20 };
+int lb_episode_log(int64_t num_envs, const uint8_t* done, const double* ep_stats, const float* reward,
+                   const int32_t* actions, float* ret32, float* ep_r32, int64_t tag, double* log, int64_t cap,
+                   uint32_t* count, void* stream);
+
 /* ---- Fused deep-sets training -----------------------------
  * Replaces the reference's autograd through the same modules in the PPO update
  * (envs/ppo_deepset.py:227-263 -> deep_sets_agent_original.py:56-106).  The training

@@ -2,8 +2,9 @@
 """Workload for the rocprofv3 PMC passes: bench.py's timed step (2^20 default envs, the
 env's random policy drawn in the kernel, obs / reward / done ring of 16, episodes staggered
 so 1/episode_length of the envs end and auto-reset every step), 16 lb_step launches after
-the stagger setup (PMC_MODE=rollout: 8 lb_rollout launches of 100 steps into a 100-deep ring, bench.py's
-default launch shape), then 3 torch copies of 1 GiB (known bytes: calibrates FETCH_SIZE /
+the stagger setup (PMC_MODE=rollout: 8 lb_rollout launches of PMC_K (default 100) steps into a
+100-deep ring -- bench.py's launch shape for its default window, PMC_K=20 for the driver's
+--steps 20 window), then 3 torch copies of 1 GiB (known bytes: calibrates FETCH_SIZE /
 WRITE_SIZE)."""
 import os
 import sys
@@ -37,8 +38,10 @@ def main():
         env.reset_masked((gid % L) == r)
     torch.cuda.synchronize()
     if rollout:
+        K = int(os.environ.get("PMC_K", T))
         for i in range(8):
-            env.rollout("random", T, obs_out=ring, reward_out=rew, done_out=done)
+            s = (i * K) % (T - K + 1)
+            env.rollout("random", K, obs_out=ring[s], reward_out=rew[s], done_out=done[s])
     else:
         for i in range(16):
             env.step_device(None, obs_out=ring[i % T], reward_out=rew[i % T], done_out=done[i % T])

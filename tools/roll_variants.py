@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Interleaved in-process A/B of lb_rollout kernel variants on bench.py's workload.
+
+    python tools/roll_variants.py [--envs N] [--steps K ...] [--variants 0,3] [--reps 3]
+
+Variants are selected in the product library with the experiment switch
+lbx_set_rollout_variant (0 k_rollout_lean OBS_DIRECT, 1 OBS_SPLIT, 2 OBS_HALVES, 3 the
+round-2 k_rollout_tpe).  The env is staggered as in bench.py (1/L of the envs finish every
+step); each measurement is ONE HIP-event pair around `launches` back-to-back K-step launches
+into the obs ring.  Prints one JSON line per (rep, K, variant).
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "gym-loadbalancing_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=1 << 20)
+    ap.add_argument("--steps", default="100,20")
+    ap.add_argument("--variants", default="3,0")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--launches", type=int, default=3)
+    ap.add_argument("--config", default="default")
+    ap.add_argument("--touch", action="store_true", help="write the whole ring once before timing")
+    ap.add_argument("--slot0", action="store_true", help="every timed launch writes from ring slot 0")
+    args = ap.parse_args()
+    import torch
+
+    import bench
+    from lbk8s import LBVecEnv, _native
+    L = _native.lib()
+    L.lbx_set_rollout_variant.argtypes = [C.c_int]
+    dev = torch.device("cuda", 0)
+    B = args.envs
+    env = LBVecEnv(B, device=dev, seed=0, as_tensors=True, **bench.CONFIGS[args.config])
+    R, EL = env.cfg.obs_rows, env.cfg.episode_length
+    T = 100
+    obs = torch.empty((T, B, R, 8), dtype=torch.float32, device=dev)
+    rew = torch.empty((T, B), dtype=torch.float32, device=dev)
+    done = torch.empty((T, B), dtype=torch.uint8, device=dev)
+    if args.touch:
+        obs.zero_()
+        rew.zero_()
+        done.zero_()
+    env.reset()
+    gid = torch.arange(B, device=dev)
+    for r in range(1, EL):
+        env.step_device(None, obs_out=obs[0], reward_out=rew[0], done_out=done[0])
+        env.reset_masked((gid % EL) == r)
+    stream = torch.cuda.current_stream(dev)
+    for rep in range(args.reps):
+        for K in [int(x) for x in args.steps.split(",")]:
+            for var in [int(x) for x in args.variants.split(",")]:
+                L.lbx_set_rollout_variant(var)
+                env.rollout("random", K, obs_out=obs[0], reward_out=rew[0], done_out=done[0])  # warm
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for i in range(args.launches):
+                    s = 0 if args.slot0 else (i * K) % max(1, T - K + 1)
+                    env.rollout("random", K, obs_out=obs[s], reward_out=rew[s], done_out=done[s])
+                e1.record(stream)
+                torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) * 1e3 / (args.launches * K)
+                print(json.dumps({"rep": rep, "K": K, "variant": var, "envs": B, "us_per_step": round(us, 2),
+                                  "env_steps_per_s": B / us * 1e6}), flush=True)
+    L.lbx_set_rollout_variant(0)
+    assert env.status() == 0
+
+
+if __name__ == "__main__":
+    main()
