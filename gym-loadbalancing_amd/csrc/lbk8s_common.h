@@ -109,12 +109,13 @@ __device__ __forceinline__ int zcap_val(uint64_t zc, int z) { return (int)((zc >
 // ---- RNG ---------------------------------------------------------------------------
 struct U4 { uint32_t x, y, z, w; };
 
-// Philox4x32-R (Salmon, Moraes, Dror, Shaw, SC'11).  The draw map runs R = 7 rounds
-// (LB_PHILOX_ROUNDS): the paper's Philox4x32-7 passes TestU01 BigCrush, and the step kernel
-// is VALU-issue bound with Philox about half its instructions (7 rounds take
-// the 2^20-env step from ~125-130 to ~115.5 us).  The round function is pinned against the
-// Random123 philox4x32_10 known answers through the oracle at R = 10.
-#define LB_PHILOX_ROUNDS 7
+// Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11), the Random123 default and SURVEY §7's
+// choice; the round function and count are pinned by the Random123 philox4x32_10 known
+// answers through the oracle.  (Rounds 1-3 used 7 rounds; an interleaved A/B on the rollout
+// kernel measured 10 rounds within 0.4-1.5% of 7, profiles/r03_ablation.jsonl.)
+#ifndef LB_PHILOX_ROUNDS  // (an A/B build may override it: tools/roll_variants.py --lib)
+#define LB_PHILOX_ROUNDS 10
+#endif
 __device__ __forceinline__ U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                      uint32_t k0, uint32_t k1) {
 #pragma unroll

@@ -84,10 +84,10 @@ typedef struct {
 } orc_env;
 
 /* ---------------- Philox4x32-R (Salmon et al., SC'11) -------------------- */
-/* The draw map runs ORC_PHILOX_ROUNDS = 7 (Philox4x32-7, BigCrush-clean per the paper);
- * orc_philox_r exposes the round count so tests pin the round function against the
- * Random123 philox4x32_10 known answers at R = 10. */
-#define ORC_PHILOX_ROUNDS 7
+/* The draw map runs ORC_PHILOX_ROUNDS = 10 (Philox4x32-10, the Random123 default);
+ * orc_philox_r exposes the round count so tests pin it against the Random123
+ * philox4x32_10 known answers. */
+#define ORC_PHILOX_ROUNDS 10
 static void philox4x32_r(uint32_t ctr[4], uint32_t k0, uint32_t k1, int rounds, uint32_t out[4]) {
     uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
     for (int i = 0; i < rounds; ++i) {

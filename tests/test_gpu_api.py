@@ -273,6 +273,7 @@ def test_vecmonitor_file_during_training(tmp_path):
     (40000, dict(num_endpoints=6), "tpe"),                                     # k_rollout_tpe, 64-thread blocks
     (70000, {}, "tpe"),                                                        # k_rollout_tpe, 256-thread blocks
     (40000, dict(num_nodes=100), "tpe"),                                       # N > 64: K policy + step launches
+    (70000, dict(auto_reset=False), "tpe"),      # k_rollout_tpe without auto-reset, envs stepped past L
 ])
 @pytest.mark.parametrize("kind", ["random", "topo", "zone_cpu", "endpoint_cpu"])
 def test_rollout_equals_policy_plus_step(B, kw, geometry, kind):
@@ -352,11 +353,15 @@ def test_rollout_tpe_staggered_equals_policy_plus_step(B, kw, kind, K, L):
     assert a_env.status() == 0
 
 
-def test_run_baselines_greedy_matches_oracle(oracle_mod):
+def test_run_baselines_greedy_matches_oracle(oracle_mod, tmp_path):
     """Config 1 driver (run_baselines.py): one launch per 100-step episode batch; every
-    episode's return and final accumulators equal the oracle's greedy episodes."""
-    from lbk8s.info import ST_RETURN
-    from lbk8s.run_baselines import CFG1, run_baselines
+    episode's return and final accumulators equal the oracle's greedy episodes, and so do the
+    per-episode CSV rows the reference's env appends (loadbalancer_k8s_env.py:488-510), as
+    written to <i>_<policy>_baselines_num_endpoints_<e>.csv and no_cost_updated.csv."""
+    import csv
+
+    from lbk8s.info import CSV_FIELDS, ST_RETURN, csv_rows
+    from lbk8s.run_baselines import CFG1, baseline_file_name, run_baselines, write_csvs
     n = 512
     for kind in ("topo", "zone_cpu", "endpoint_cpu"):
         res = run_baselines(kind, n, seed=42)
@@ -366,5 +371,18 @@ def test_run_baselines_greedy_matches_oracle(oracle_mod):
         for s in range(CFG1["episode_length"]):
             _, r, _, _, _ = orc.step(orc.policy_greedy(kind))
             np.testing.assert_array_equal(res["rewards"][s], r)
-        np.testing.assert_array_equal(res["returns"], orc.stats()[:, ST_RETURN])
+        st = orc.stats()
+        np.testing.assert_array_equal(res["returns"], st[:, ST_RETURN])
         assert (res["returns"] == 100).all()  # greedy never rejects (masks all True), naive +1
+        name = baseline_file_name(0, kind, 6)
+        write_csvs(res, name, str(tmp_path))
+        for fname, col in ((name + ".csv", 0), ("no_cost_updated.csv", 1)):
+            with open(tmp_path / fname) as f:
+                rows = list(csv.DictReader(f, fieldnames=list(CSV_FIELDS)))
+            rows = rows[-n:]  # no_cost_updated.csv is shared by the three policies (append)
+            assert len(rows) == n
+            for i in (0, 1, n // 2, n - 1):
+                exp = csv_rows(st[i], i + 1)[col]
+                got = rows[i]
+                for k in CSV_FIELDS[:-1]:  # (execution_time is wall clock)
+                    assert float(got[k]) == float(exp[k]), (fname, i, k)

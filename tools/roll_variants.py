@@ -28,12 +28,15 @@ def main():
     ap.add_argument("--launches", type=int, default=3)
     ap.add_argument("--config", default="default")
     ap.add_argument("--touch", action="store_true", help="write the whole ring once before timing")
+    ap.add_argument("--lib", default=None, help="another build of liblbk8s.so (an A/B across builds)")
     ap.add_argument("--slot0", action="store_true", help="every timed launch writes from ring slot 0")
     args = ap.parse_args()
     import torch
 
     import bench
     from lbk8s import LBVecEnv, _native
+    if args.lib:
+        _native.LIB_PATH = os.path.abspath(args.lib)
     L = _native.lib()
     L.lbx_set_rollout_variant.argtypes = [C.c_int]
     dev = torch.device("cuda", 0)
@@ -67,9 +70,11 @@ def main():
                     env.rollout("random", K, obs_out=obs[s], reward_out=rew[s], done_out=done[s])
                 e1.record(stream)
                 torch.cuda.synchronize()
-                us = e0.elapsed_time(e1) * 1e3 / (args.launches * K)
-                print(json.dumps({"rep": rep, "K": K, "variant": var, "envs": B, "us_per_step": round(us, 2),
-                                  "env_steps_per_s": B / us * 1e6}), flush=True)
+                us_launch = e0.elapsed_time(e1) * 1e3 / args.launches
+                us = us_launch / max(K, 1)
+                print(json.dumps({"rep": rep, "K": K, "variant": var, "lib": os.path.basename(_native.LIB_PATH),
+                                  "envs": B, "us_per_launch": round(us_launch, 2), "us_per_step": round(us, 2),
+                                  "env_steps_per_s": B * K / us_launch * 1e6}), flush=True)
     L.lbx_set_rollout_variant(0)
     assert env.status() == 0
 
