@@ -38,6 +38,10 @@
 
 namespace lbk {
 
+#ifdef LB_TIMELINE
+__device__ uint64_t* g_timeline;  // [waves][K + 2] s_memrealtime (100 MHz) stamps, or NULL
+#endif
+
 // lem (the rollout's emeta register): zone[0:2) owner[2:10) type[10:13) c0[13:20) k0[20:29)
 // with k0 = trunc(lat0), the endpoint's LAT row (the node id is not needed inside the launch)
 __device__ __forceinline__ int lem_k0(uint32_t m) { return (int)(m >> 20); }
@@ -81,44 +85,62 @@ struct LDims {
 };
 
 // ---- k_rollout_img's per-env LDS image (IMG_W words, odd: conflict-free per-lane writes)
-//   [0] dt (f32)   [1] topo(rz, zone 0) | topo(rz, zone 1) << 9 | rz << 18 | thr_idx << 20
-//   [2] topo(rz, zone 2) | topo(rz, zone 3) << 9
-//   [IMG_EP + 3e] zone | zone_cpu_capacity << 2   [+1] cpu (f32)   [+2] latency (f32)
-// The endpoint words change only when the endpoint is selected (2 words) or an episode
-// starts; the request words every step (3 words).  The copy-out decodes the rows from it.
-constexpr int IMG_EP = 3, IMG_W = IMG_EP + 3 * TPE_E;  // 27
+//   [0] req_zone (f32)   [1] threshold (f32)   [2] dt (f32)
+//   [IMG_EP + 4e]: zone | zone_cpu_capacity << 2,  cpu (f32),  latency (f32),  topology
+//                  latency to the request's zone (f32)
+// The endpoint's first three words change only when it is selected (2 words) or an episode
+// starts; the request words and the topology column every step.  A float4 piece of the obs
+// rows is then 4 LDS words and no arithmetic but the zone / capacity conversion.
+constexpr int IMG_EP = 3, IMG_W = IMG_EP + 4 * TPE_E;  // 35
 
-__device__ __forceinline__ void img_request(uint32_t* me, const LEnv& v) {
+__device__ __forceinline__ void img_request(uint32_t* me, const LEnv& v, const uint32_t (&em)[TPE_E], int E) {
     const int rz = (int)((v.s1 >> S1_RZ) & 3);
-    const uint32_t t0 = (uint32_t)topo_val(v.topo, 0, rz), t1 = (uint32_t)topo_val(v.topo, 1, rz);
-    const uint32_t t2 = (uint32_t)topo_val(v.topo, 2, rz), t3 = (uint32_t)topo_val(v.topo, 3, rz);
-    me[0] = __float_as_uint(v.dt);
-    me[1] = t0 | (t1 << 9) | ((v.s1 >> S1_RZ) & 0x1Fu) << 18;  // rz, thr_idx
-    me[2] = t2 | (t3 << 9);
+    const float t0 = (float)topo_val(v.topo, 0, rz), t1 = (float)topo_val(v.topo, 1, rz);
+    const float t2 = (float)topo_val(v.topo, 2, rz), t3 = (float)topo_val(v.topo, 3, rz);
+    me[0] = __float_as_uint((float)rz);
+    me[1] = __float_as_uint((float)threshold((int)((v.s1 >> S1_THR) & 7)));
+    me[2] = __float_as_uint(v.dt);
+#pragma unroll
+    for (int e = 0; e < TPE_E; ++e) {
+        if (e >= E) continue;
+        const int z = em_zone(em[e]);
+        const float t = z == 0 ? t0 : (z == 1 ? t1 : (z == 2 ? t2 : t3));
+        me[IMG_EP + 4 * e + 3] = __float_as_uint(t);
+    }
 }
-// piece j (row j / 2, half j % 2) of one env's rows from its image
+// piece j (row j / 2, half j % 2) of one env's rows from its image, without branches (the
+// lanes of one store hold both halves; the reject row's -1s are blended in bitwise)
 __device__ __forceinline__ float4 img_piece(const uint32_t* b, int j, int E) {
-    const int row = j >> 1, half = j & 1;
-    const int rr = row < E ? row : 0;
-    const uint32_t A = b[IMG_EP + 3 * rr + (half ? 2 : 0)];  // latency | zone word
-    const uint32_t C = b[IMG_EP + 3 * rr + 1];               // cpu
-    const uint32_t H1 = b[1], H2 = b[2], D = b[0];
-    const int zone = (int)(A & 3);
-    const uint32_t tw = zone < 2 ? H1 : H2;
-    const float topo = (float)((tw >> (9 * (zone & 1))) & 0x1FF);
-    const float rz = (float)((H1 >> 18) & 3), thr = (float)threshold((int)((H1 >> 20) & 7));
-    float4 o;
-    if (half) o = make_float4(row < E ? __uint_as_float(A) : -1.f, rz, thr, __uint_as_float(D));
-    else o = row < E ? make_float4((float)zone, (float)(A >> 2), __uint_as_float(C), topo) : make_float4(-1.f, -1.f, -1.f, -1.f);
-    return o;
+    const int row = j >> 1;
+    const bool half = (j & 1) != 0, rej = row >= E;
+    const uint32_t* ep = b + IMG_EP + 4 * (rej ? 0 : row);
+    const uint32_t r0 = half ? ep[2] : ep[0];  // latency | zone word
+    const uint32_t r1 = half ? b[0] : ep[1];   // req_zone | cpu
+    const uint32_t r2 = half ? b[1] : ep[3];   // threshold | topology
+    const uint32_t r3 = b[2];                  // dt
+    const uint32_t x = half ? r0 : __float_as_uint((float)(r0 & 3));
+    const uint32_t y = half ? r1 : __float_as_uint((float)(r0 >> 2));
+    const uint32_t z = half ? r2 : r1;
+    const uint32_t w = half ? r3 : r2;
+    const uint32_t NEG = 0xBF800000u;                 // -1.f
+    const uint32_t mx = rej ? ~0u : 0u;               // reject row: x = -1
+    const uint32_t my = (rej && !half) ? ~0u : 0u;    // its first half: all -1
+    return make_float4(__uint_as_float((mx & NEG) | (~mx & x)), __uint_as_float((my & NEG) | (~my & y)),
+                       __uint_as_float((my & NEG) | (~my & z)), __uint_as_float((my & NEG) | (~my & w)));
 }
 
 // the next step's action (policy on the current state), its selected endpoint's 4 table
 // values (the lat0 of a first selection instead of LAT[0]) and its request draws
-template <int KIND, int ET, int RT>
+// between(stage), stage = 0..PREP_STAGES-1, runs between the stages of the computation (the
+// rollout issues the previous step's obs stores there, so they spread over the step's work)
+constexpr int PREP_STAGES = 6;
+struct NoInterleave {
+    __device__ __forceinline__ void operator()(int) const {}
+};
+template <int KIND, int ET, int RT, typename F = NoInterleave>
 __device__ __forceinline__ LPrep lean_prep(const Params& p, const LDims<ET, RT>& d, int64_t ev, const LEnv& v,
                                            const uint32_t (&em)[TPE_E], const uint32_t (&ed)[TPE_E],
-                                           uint32_t l0off, uint32_t l0step) {
+                                           uint32_t l0off, uint32_t l0step, F&& between = F()) {
     LPrep r;
     TEnv tv;  // the policy's view (tpe_policy)
     tv.topo = v.topo;
@@ -128,6 +150,7 @@ __device__ __forceinline__ LPrep lean_prep(const Params& p, const LDims<ET, RT>&
     tv.s.step = (int)(v.s0 & 0xFFFF);
     const int a = tpe_policy<KIND>(p, ev, tv, em, ed);
     r.a = a;
+    between(0);
     const int E = d.E;
     const bool accept = a >= -E && a < E;
     const int ai = accept ? (a < 0 ? a + E : a) : 0;
@@ -151,18 +174,23 @@ __device__ __forceinline__ LPrep lean_prep(const Params& p, const LDims<ET, RT>&
     r.sel_cpu = *at(p.lat_lut, cpu0 + (uint32_t)(ed_m(edA) * CPU_ROWS + c0A) * 8u);
     r.next_lat = *at(p.lat_lut, (uint32_t)(jn * LAT_ROWS + k0A) * 8u);
     r.next_cpu = *at(p.lat_lut, cpu0 + (uint32_t)(Mn * CPU_ROWS + c0A) * 8u);
+    between(1);
     const int step = (int)(v.s0 & 0xFFFF);
     // next_request()'s draws (tpe_request_draws' map), the two float64 logs one after the
     // other: interleaved they held two log chains' temporaries at once
     const uint32_t episode = (uint32_t)(v.acc3 >> 32), slot = (uint32_t)(step + 1);
     const U4 wx = draw(p, ev, episode, slot, D_REQ_X);
+    between(2);
     r.x1 = p.inv_rate * std_exp(wx.x, wx.y);
     __builtin_amdgcn_sched_barrier(0);
+    between(3);
     r.x2 = p.call * std_exp(wx.z, wx.w);
     __builtin_amdgcn_sched_barrier(0);
+    between(4);
     const U4 wi = draw(p, ev, episode, slot, D_REQ_I);
     r.r = (int)bounded(wi.x, 7);
     r.n = (int)bounded(wi.y, (uint32_t)p.N);
+    between(5);
     return r;
 }
 
@@ -212,8 +240,8 @@ __device__ __forceinline__ double lean_apply(const Params& p, const LDims<ET, RT
             const uint32_t edo = e == oA ? (ed[e] & ~(0x3FFu << 20)) | ((uint32_t)Mn << 20) : ed[e];
             ed[e] = e == ai ? edA_new : edo;
         }
-        me[IMG_EP + 3 * ai + 1] = __float_as_uint((float)pr.next_cpu);
-        me[IMG_EP + 3 * ai + 2] = __float_as_uint((float)pr.next_lat);
+        me[IMG_EP + 4 * ai + 1] = __float_as_uint((float)pr.next_cpu);
+        me[IMG_EP + 4 * ai + 2] = __float_as_uint((float)pr.next_lat);
         v.s1 &= ~(1u << S1_PEN);
         reward = accept_reward(p, pr.sel_lat, tl, pr.sel_cpu, v.acc2, (int)(v.s0 >> 16));
         v.last_r = reward;
@@ -233,7 +261,7 @@ __device__ __forceinline__ double lean_apply(const Params& p, const LDims<ET, RT
     const uint64_t word = pr.n < 32 ? v.nz0 : v.nz1;
     const uint32_t rz = (uint32_t)((word >> (2 * (pr.n & 31))) & 3);
     v.s1 = (v.s1 & ~((3u << S1_RZ) | (7u << S1_THR))) | (rz << S1_RZ) | ((uint32_t)((pr.r + 6) % 7) << S1_THR);
-    img_request(me, v);
+    img_request(me, v, em, E);
     return reward;
 }
 
@@ -259,30 +287,59 @@ __device__ __forceinline__ void img_endpoints(uint32_t* me, const LDims<ET, RT>&
     for (int e = 0; e < TPE_E; ++e) {
         if (e >= d.E) continue;
         const int z = em_zone(em[e]);
-        me[IMG_EP + 3 * e] = (uint32_t)z | ((uint32_t)zcap_val(zcap, z) << 2);
-        me[IMG_EP + 3 * e + 1] = __float_as_uint(cpu[e]);
-        me[IMG_EP + 3 * e + 2] = __float_as_uint(lat[e]);
+        me[IMG_EP + 4 * e] = (uint32_t)z | ((uint32_t)zcap_val(zcap, z) << 2);
+        me[IMG_EP + 4 * e + 1] = __float_as_uint(cpu[e]);
+        me[IMG_EP + 4 * e + 2] = __float_as_uint(lat[e]);
     }
 }
 
-// the wave's rows from its image into out (the wave's block of 64 envs x P float4):
-// FLAGGED = only the envs whose bit is set in m (their runs; iterations holding none skipped)
-template <bool FLAGGED>
-__device__ __forceinline__ void img_copy_out(const uint32_t* wimg, float4* outw, int nenv, int P, int E, int lane,
+// the wave's rows from its image into out (the wave's block of 64 envs x P float4): store
+// instruction it covers pieces q = 64 it + lane, env q / P, piece q % P (PT = P when it is a
+// compile-time constant: the loop unrolls in pairs and the FLAGGED spans are constants).
+// FLAGGED = only the envs whose bit is set in m (their runs; stores holding none skipped).
+template <bool FLAGGED, int PT>
+__device__ __forceinline__ void img_copy_out(const uint32_t* wimg, float4* outw, int nenv, int P_, int E, int lane,
                                              uint64_t m) {
+    const int P = PT > 0 ? PT : P_;
     const int del = 64 / P, dj = 64 - del * P;
-    int el = lane / P, j = lane - (lane / P) * P;
+    // (opaque per call: the pieces' LDS addresses depend on the lane only, and hoisting all 2R
+    // of them out of the step loop would hold them in registers across the whole launch)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    int el = ln / P, j = ln - (ln / P) * P;
 #pragma unroll 1
     for (int it = 0; it < P; ++it) {
         bool go = el < nenv;
         if constexpr (FLAGGED) {
             const int lo = (64 * it) / P, hi = (64 * it + 63) / P;  // envs this store touches
             const uint64_t span = (hi >= 63 ? ~0ull : ((2ull << hi) - 1)) & ~((1ull << lo) - 1);
-            if (!(m & span)) goto next;  // uniform
-            go = go && ((m >> el) & 1);
+            go = go && (m & span) && ((m >> el) & 1);
         }
         if (go) st_stream(outw + 64 * it + lane, img_piece(wimg + el * IMG_W, j, E));
-    next:
+        el += del;
+        j += dj;
+        if (j >= P) { j -= P; ++el; }
+    }
+}
+
+// The wave's obs stores [it0, it1) (store it = pieces 64 it .. 64 it + 63), branch-free: a
+// lane past the last live env (a partial last wave) repeats the last env's piece j, i.e. the
+// same value to the same address as the lane that owns it.  elj = the lane's (env, piece) at
+// it = 0 (el | j << 8).
+__device__ __forceinline__ void img_copy_range(const uint32_t* wimg, float4* outw, int nenv, int P, int E, int lane,
+                                               int elj, int it0, int it1) {
+    const int del = 64 / P, dj = 64 - del * P;
+    // (opaque per call: the pieces' LDS addresses depend on the lane only, and hoisting them
+    // out of the step loop would hold 2R of them in registers across the whole launch)
+    asm volatile("" : "+v"(elj));
+    int el = elj & 0xFF, j = elj >> 8;
+    // position at it0 (it0 * 64 pieces further)
+    const int q = 64 * it0 + el * P + j;
+    el = q / P;
+    j = q - el * P;
+    for (int it = it0; it < it1; ++it) {
+        const int ec = el < nenv ? el : nenv - 1;
+        st_stream(outw + (int64_t)ec * P + j, img_piece(wimg + ec * IMG_W, j, E));
         el += del;
         j += dj;
         if (j >= P) { j -= P; ++el; }
@@ -311,9 +368,9 @@ __device__ __forceinline__ void img_start_episode(const Params& p, const LDims<E
             const double l0 = __longlong_as_double((long long)((uint64_t)lw[2 * i] | ((uint64_t)lw[2 * i + 1] << 32)));
             em[e] = lem_make(mw[i], l0);
             const int z = em_zone(mw[i]);
-            me[IMG_EP + 3 * e] = (uint32_t)z | ((uint32_t)zcap_val(zcap, z) << 2);
-            me[IMG_EP + 3 * e + 1] = __float_as_uint((float)em_c0(mw[i]));  // table rows 0: the initial values
-            me[IMG_EP + 3 * e + 2] = __float_as_uint((float)l0);
+            me[IMG_EP + 4 * e] = (uint32_t)z | ((uint32_t)zcap_val(zcap, z) << 2);
+            me[IMG_EP + 4 * e + 1] = __float_as_uint((float)em_c0(mw[i]));  // table rows 0: the initial values
+            me[IMG_EP + 4 * e + 2] = __float_as_uint((float)l0);
         }
     }
     (void)rw;
@@ -338,11 +395,12 @@ __device__ __forceinline__ void img_start_episode(const Params& p, const LDims<E
     const double departure = arrival + x2;
     v.dt = (float)(departure - arrival);
     v.t = arrival;
-    img_request(me, v);
+    img_request(me, v, em, d.E);
 }
 
 template <int NB, int KIND, int ET, int RT, int MINW = 1>
-__global__ __launch_bounds__(NB, MINW) void k_rollout_img(Params p, int K, int32_t* act_out) {
+__global__ __launch_bounds__(NB, MINW) void k_rollout_img(Params p, int K, int32_t* act_out, int stagger,
+                                                          int resident_blocks) {
     constexpr int NW = NB / 64;
     __shared__ uint32_t simg[NW][64 * IMG_W];
     const LDims<ET, RT> d(p);
@@ -355,6 +413,7 @@ __global__ __launch_bounds__(NB, MINW) void k_rollout_img(Params p, int K, int32
     const int64_t ev = live ? env : 0;  // dead lanes step env 0's copy and store nothing
     const int E = d.E, R = d.R, P = 2 * R;
     const int nenv = p.B - env0 < 64 ? (int)(p.B - env0) : 64;
+    const int elj = (lane / (2 * R)) | ((lane % (2 * R)) << 8);  // the lane's first obs piece
 
     // first (with nothing else live), the next episodes of the envs that end inside the
     // launch, into their records (8 lanes per env); the list lives in the image region
@@ -428,7 +487,20 @@ __global__ __launch_bounds__(NB, MINW) void k_rollout_img(Params p, int K, int32
     const int64_t obs_slot = p.B * (int64_t)R * 8;
 
     LPrep pr = lean_prep<KIND>(p, d, ev, v, em, ed, l0off, l0step);
+    // The first generation of blocks starts in lockstep: every wave computes, then every wave
+    // stores, and the compute and store phases of a step do not overlap until the waves drift
+    // apart.  Staggering the first generation's blocks (later generations start as earlier
+    // blocks finish, already staggered) gives that overlap from the first step.
+    if ((int)blockIdx.x < resident_blocks)
+        for (int s = 0; s < stagger * (int)(blockIdx.x & 3); ++s) __builtin_amdgcn_s_sleep(127);
+#ifdef LB_TIMELINE  // diagnostic build (tools/timeline.py): each wave's step start times
+    const int64_t gw = (int64_t)blockIdx.x * NW + wv;
+    if (g_timeline && lane == 0) g_timeline[gw * (K + 2)] = __builtin_amdgcn_s_memrealtime();
+#endif
     for (int k = 0; k < K; ++k) {
+#ifdef LB_TIMELINE
+        if (g_timeline && lane == 0) g_timeline[gw * (K + 2) + 1 + k] = __builtin_amdgcn_s_memrealtime();
+#endif
         if (act_out && live) *at(act_out + (int64_t)k * p.B, envi * 4u) = pr.a;
         v.s0 += 1;  // step (<= L: the episode ends there)
         const bool done = live && (int)(v.s0 & 0xFFFF) == p.L;  // (:472)
@@ -444,7 +516,7 @@ __global__ __launch_bounds__(NB, MINW) void k_rollout_img(Params p, int K, int32
                                 v.total, v.sum_lat, v.sum_cpu, v.sum_hi);
             if (p.term_obs) {
                 wave_lds_sync();
-                img_copy_out<true>(wimg, reinterpret_cast<float4*>(p.term_obs) + env0 * P, nenv, P, E, lane, m);
+                img_copy_out<true, 2 * RT>(wimg, reinterpret_cast<float4*>(p.term_obs) + env0 * P, nenv, P, E, lane, m);
             }
             if (done) {
                 wave_lds_sync();  // (the copy-out read the terminal image)
@@ -454,13 +526,26 @@ __global__ __launch_bounds__(NB, MINW) void k_rollout_img(Params p, int K, int32
                 l0step = 8u;
             }
         }
-        if (k + 1 < K) pr = lean_prep<KIND>(p, d, ev, v, em, ed, l0off, l0step);
-        if (p.obs) {
-            wave_lds_sync();
-            img_copy_out<false>(wimg, reinterpret_cast<float4*>(p.obs + k * obs_slot) + env0 * P, nenv, P, E, lane, 0);
-            wave_lds_sync();  // (the next step rewrites the image)
+        // step k's obs rows leave while step k + 1's action, gathers and draws are computed:
+        // the stores of a wave spread over its step instead of one burst at the end
+        float4* outw = p.obs ? reinterpret_cast<float4*>(p.obs + k * obs_slot) + env0 * P : nullptr;
+        if (outw) wave_lds_sync();
+        auto stores = [&](int stage) {
+            if (!outw) return;
+            const int per = (P + PREP_STAGES - 1) / PREP_STAGES;
+            const int it0 = stage * per, it1 = it0 + per < P ? it0 + per : P;
+            img_copy_range(wimg, outw, nenv, P, E, lane, elj, it0, it1);
+        };
+        if (k + 1 < K) {
+            pr = lean_prep<KIND>(p, d, ev, v, em, ed, l0off, l0step, stores);
+        } else {
+            for (int st = 0; st < PREP_STAGES; ++st) stores(st);
         }
+        if (outw) wave_lds_sync();  // (the next step rewrites the image)
     }
+#ifdef LB_TIMELINE
+    if (g_timeline && lane == 0) g_timeline[gw * (K + 2) + K + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
     if (!live) return;
 #pragma unroll
     for (int e = 0; e < TPE_E; ++e)

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--config", default="default")
     ap.add_argument("--touch", action="store_true", help="write the whole ring once before timing")
     ap.add_argument("--lib", default=None, help="another build of liblbk8s.so (an A/B across builds)")
+    ap.add_argument("--staggers", default="", help="k_rollout_img first-generation stagger values to sweep")
+    ap.add_argument("--no-obs", action="store_true", help="launch without the obs output (compute + small outputs)")
     ap.add_argument("--slot0", action="store_true", help="every timed launch writes from ring slot 0")
     args = ap.parse_args()
     import torch
@@ -39,6 +41,8 @@ def main():
         _native.LIB_PATH = os.path.abspath(args.lib)
     L = _native.lib()
     L.lbx_set_rollout_variant.argtypes = [C.c_int]
+    L.lbx_set_stagger.argtypes = [C.c_int]
+    staggers = [int(x) for x in args.staggers.split(",")] if args.staggers else [None]
     dev = torch.device("cuda", 0)
     B = args.envs
     env = LBVecEnv(B, device=dev, seed=0, as_tensors=True, **bench.CONFIGS[args.config])
@@ -59,20 +63,24 @@ def main():
     stream = torch.cuda.current_stream(dev)
     for rep in range(args.reps):
         for K in [int(x) for x in args.steps.split(",")]:
-            for var in [int(x) for x in args.variants.split(",")]:
+            for var, stg in [(v, g) for v in [int(x) for x in args.variants.split(",")] for g in staggers]:
                 L.lbx_set_rollout_variant(var)
+                if stg is not None:
+                    L.lbx_set_stagger(stg)
                 env.rollout("random", K, obs_out=obs[0], reward_out=rew[0], done_out=done[0])  # warm
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
                 for i in range(args.launches):
                     s = 0 if args.slot0 else (i * K) % max(1, T - K + 1)
-                    env.rollout("random", K, obs_out=obs[s], reward_out=rew[s], done_out=done[s])
+                    env.rollout("random", K, obs_out=None if args.no_obs else obs[s], reward_out=rew[s],
+                                done_out=done[s])
                 e1.record(stream)
                 torch.cuda.synchronize()
                 us_launch = e0.elapsed_time(e1) * 1e3 / args.launches
                 us = us_launch / max(K, 1)
-                print(json.dumps({"rep": rep, "K": K, "variant": var, "lib": os.path.basename(_native.LIB_PATH),
+                print(json.dumps({"rep": rep, "K": K, "variant": var, "stagger": stg,
+                                  "lib": os.path.basename(_native.LIB_PATH),
                                   "envs": B, "us_per_launch": round(us_launch, 2), "us_per_step": round(us, 2),
                                   "env_steps_per_s": B * K / us_launch * 1e6}), flush=True)
     L.lbx_set_rollout_variant(0)
