@@ -266,8 +266,6 @@ thread_local std::string g_err;
 // experiment switch (lbx_set_rollout_variant, tools/roll_variants.py): 3 = the round-2
 // k_rollout_tpe for the L >= K launches k_rollout_img serves (an A/B reference)
 int g_rollout_variant = 0;
-// k_rollout_img's first-generation stagger: blockIdx % 4 units of 127 x 64 clocks (lbx_set_stagger)
-int g_stagger = 0;
 
 int fail(const char* msg) {
     g_err = msg;
@@ -489,7 +487,6 @@ extern "C" {
 int lb_abi_version(void) { return LBK8S_ABI_VERSION; }
 
 int lbx_set_rollout_variant(int v) { g_rollout_variant = v; return 0; }
-int lbx_set_stagger(int v) { g_stagger = v; return 0; }
 #ifdef LB_TIMELINE
 int lbx_set_timeline(uint64_t* buf) { return hipMemcpyToSymbol(HIP_SYMBOL(g_timeline), &buf, sizeof(buf)) == hipSuccess ? 0 : -1; }
 #endif
@@ -624,26 +621,10 @@ int lb_rollout(void* state, const lb_config* cfg, int64_t num_envs, int32_t poli
         const bool pre = cfg->auto_reset && cfg->episode_length >= steps;
         if (pre && g_rollout_variant != 3) {  // k_rollout_img (lbk8s_rollout.h)
             const bool e8 = p.E == 8 && p.R == 9;
-            const int resident = device_cus() * (small ? 16 : 4);  // blocks of the first generation
 #define LB_IMG(NB_, KIND_)                                                                                   \
-            if (e8) hipLaunchKernelGGL((k_rollout_img<NB_, KIND_, 8, 9, 4>), grid, block, 0, s, p, (int)steps, actions_out, \
-                                       g_stagger, resident);                                                     \
-            else hipLaunchKernelGGL((k_rollout_img<NB_, KIND_, 0, 0, 4>), grid, block, 0, s, p, (int)steps, actions_out, \
-                                    g_stagger, resident);
+            if (e8) hipLaunchKernelGGL((k_rollout_img<NB_, KIND_, 8, 9, 4>), grid, block, 0, s, p, (int)steps, actions_out); \
+            else hipLaunchKernelGGL((k_rollout_img<NB_, KIND_, 0, 0, 4>), grid, block, 0, s, p, (int)steps, actions_out);
 #define LB_IMG_KIND(KIND_) if (small) { LB_IMG(64, KIND_) } else { LB_IMG(BLOCK, KIND_) }
-            if (e8 && policy == LB_POLICY_RANDOM && g_rollout_variant >= 8) {  // shape experiments
-                const dim3 g64((unsigned)((num_envs + 63) / 64)), b64(64);
-                if (g_rollout_variant == 8)
-                    hipLaunchKernelGGL((k_rollout_img<64, LB_POLICY_RANDOM, 8, 9, 4>), g64, b64, 0, s, p, (int)steps,
-                                       actions_out, g_stagger, device_cus() * 16);
-                else if (g_rollout_variant == 9)
-                    hipLaunchKernelGGL((k_rollout_img<BLOCK, LB_POLICY_RANDOM, 8, 9, 1>), grid, block, 0, s, p, (int)steps,
-                                       actions_out, g_stagger, resident);
-                else
-                    hipLaunchKernelGGL((k_rollout_img<64, LB_POLICY_RANDOM, 8, 9, 1>), g64, b64, 0, s, p, (int)steps,
-                                       actions_out, g_stagger, device_cus() * 12);
-                return check_launch();
-            }
             switch (policy) {
             case LB_POLICY_TOPOLOGY_GREEDY: LB_IMG_KIND(LB_POLICY_TOPOLOGY_GREEDY); break;
             case LB_POLICY_ZONE_CPU_GREEDY: LB_IMG_KIND(LB_POLICY_ZONE_CPU_GREEDY); break;

@@ -399,8 +399,7 @@ __device__ __forceinline__ void img_start_episode(const Params& p, const LDims<E
 }
 
 template <int NB, int KIND, int ET, int RT, int MINW = 1>
-__global__ __launch_bounds__(NB, MINW) void k_rollout_img(Params p, int K, int32_t* act_out, int stagger,
-                                                          int resident_blocks) {
+__global__ __launch_bounds__(NB, MINW) void k_rollout_img(Params p, int K, int32_t* act_out) {
     constexpr int NW = NB / 64;
     __shared__ uint32_t simg[NW][64 * IMG_W];
     const LDims<ET, RT> d(p);
@@ -487,12 +486,6 @@ __global__ __launch_bounds__(NB, MINW) void k_rollout_img(Params p, int K, int32
     const int64_t obs_slot = p.B * (int64_t)R * 8;
 
     LPrep pr = lean_prep<KIND>(p, d, ev, v, em, ed, l0off, l0step);
-    // The first generation of blocks starts in lockstep: every wave computes, then every wave
-    // stores, and the compute and store phases of a step do not overlap until the waves drift
-    // apart.  Staggering the first generation's blocks (later generations start as earlier
-    // blocks finish, already staggered) gives that overlap from the first step.
-    if ((int)blockIdx.x < resident_blocks)
-        for (int s = 0; s < stagger * (int)(blockIdx.x & 3); ++s) __builtin_amdgcn_s_sleep(127);
 #ifdef LB_TIMELINE  // diagnostic build (tools/timeline.py): each wave's step start times
     const int64_t gw = (int64_t)blockIdx.x * NW + wv;
     if (g_timeline && lane == 0) g_timeline[gw * (K + 2)] = __builtin_amdgcn_s_memrealtime();

@@ -4,8 +4,8 @@
     python tools/roll_variants.py [--envs N] [--steps K ...] [--variants 0,3] [--reps 3]
 
 Variants are selected in the product library with the experiment switch
-lbx_set_rollout_variant (0 k_rollout_lean OBS_DIRECT, 1 OBS_SPLIT, 2 OBS_HALVES, 3 the
-round-2 k_rollout_tpe).  The env is staggered as in bench.py (1/L of the envs finish every
+lbx_set_rollout_variant (0 the product dispatch, k_rollout_img; 3 the round-2
+k_rollout_tpe).  The env is staggered as in bench.py (1/L of the envs finish every
 step); each measurement is ONE HIP-event pair around `launches` back-to-back K-step launches
 into the obs ring.  Prints one JSON line per (rep, K, variant).
 """
@@ -29,7 +29,6 @@ def main():
     ap.add_argument("--config", default="default")
     ap.add_argument("--touch", action="store_true", help="write the whole ring once before timing")
     ap.add_argument("--lib", default=None, help="another build of liblbk8s.so (an A/B across builds)")
-    ap.add_argument("--staggers", default="", help="k_rollout_img first-generation stagger values to sweep")
     ap.add_argument("--no-obs", action="store_true", help="launch without the obs output (compute + small outputs)")
     ap.add_argument("--slot0", action="store_true", help="every timed launch writes from ring slot 0")
     args = ap.parse_args()
@@ -41,8 +40,7 @@ def main():
         _native.LIB_PATH = os.path.abspath(args.lib)
     L = _native.lib()
     L.lbx_set_rollout_variant.argtypes = [C.c_int]
-    L.lbx_set_stagger.argtypes = [C.c_int]
-    staggers = [int(x) for x in args.staggers.split(",")] if args.staggers else [None]
+    staggers = [None]
     dev = torch.device("cuda", 0)
     B = args.envs
     env = LBVecEnv(B, device=dev, seed=0, as_tensors=True, **bench.CONFIGS[args.config])
@@ -65,8 +63,6 @@ def main():
         for K in [int(x) for x in args.steps.split(",")]:
             for var, stg in [(v, g) for v in [int(x) for x in args.variants.split(",")] for g in staggers]:
                 L.lbx_set_rollout_variant(var)
-                if stg is not None:
-                    L.lbx_set_stagger(stg)
                 env.rollout("random", K, obs_out=obs[0], reward_out=rew[0], done_out=done[0])  # warm
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
