@@ -307,22 +307,32 @@ def main(argv=None):
         model = f"lb_rollout: {out_b} + {b_step - out_b}/k B per env-step, k = {launches[0] if len(set(launches)) == 1 else launches} steps per launch"
     achieved = b_alg * B / (kernel_ms * 1e-3) / 1e9
     traffic = None
-    pmc_path = args.pmc_json if args.launch == "step" else args.pmc_json.replace(".json", "_rollout.json")
-    try:
-        with open(pmc_path) as f:
-            pmc = json.load(f)
-        # only a PMC pass of the same launch shape (config, envs, steps per launch) prices this line
+    # PMC passes per launch shape: pmc_traffic.json (lb_step), pmc_traffic_rollout_k{K}.json
+    # (lb_rollout launches of K steps); only a pass of the same shape (config, envs, steps per
+    # launch) prices this line, otherwise traffic is null
+    if args.launch == "step":
+        pmc_paths = [args.pmc_json]
+    else:
+        pmc_paths = [args.pmc_json.replace(".json", f"_rollout_k{launches[0]}.json"),
+                     args.pmc_json.replace(".json", "_rollout.json")]
+    pmc_file = None
+    for pmc_path in pmc_paths:
+        try:
+            with open(pmc_path) as f:
+                pmc = json.load(f)
+        except (OSError, ValueError):
+            continue
         if (pmc.get("config") == args.config and pmc.get("envs") == B and len(set(launches)) == 1
                 and pmc.get("steps_per_launch", 1) == launches[0]):
             traffic = pmc.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
+            pmc_file = os.path.relpath(pmc_path, REPO)
+            break
     tpe = env.cfg.num_endpoints <= 8 and (args.geometry == "tpe" or (args.geometry == "auto" and B >= 32768))
     if args.launch == "step":
         kname = "k_step_tpe (lb_step, auto-reset inside)" if tpe else "k_step_slice (lb_step)"
     else:
-        kname = (f"k_rollout_lean (lb_rollout, random policy, auto-reset inside)" if tpe
-                 else f"k_rollout_slice (lb_rollout)")
+        kname = ("k_rollout_img (lb_rollout, random policy, auto-reset inside)" if tpe
+                 else "k_rollout_slice (lb_rollout)")
     line = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": K,
         "warmup": args.warmup, "ms_per_step": el / K * 1e3, "higher_is_better": True,
@@ -338,7 +348,7 @@ def main(argv=None):
                    "resets_in_window": resets, "graphs": res["graphs"], "geometry": args.geometry,
                    "launch": args.launch, "parallelism": f"env-sharded x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": pmc_file, "kernel": kname,
                      "kernel_ms": kernel_ms, "bytes_per_env_step": b_alg, "byte_model": model,
                      "envs_per_launch": B, "launches_timed": n_launch, "steps_per_launch": k_avg,
                      # one launch = steps_per_launch vector steps: the rocprof average duration
