@@ -5,7 +5,7 @@
 // One lane = one env for all K steps of the launch, as k_rollout_tpe (lbk8s_tpe.h), laid out
 // for occupancy.  k_rollout_tpe held the whole env in registers (178-190 VGPRs) and staged all
 // 64 envs' rows in LDS every step (78 KB per block): two waves per SIMD, 2^20 envs in eight
-// block generations.  Here (127 VGPRs, 27 KB per block: four waves per SIMD, four generations)
+// block generations.  Here (128 VGPRs, 40 KB per block: four waves per SIMD, four generations)
 //   * the endpoints' initial latencies (16 VGPRs) are not held: a step needs lat0 only when
 //     it selects an endpoint for the first time, and then gathers it (from the state's lat0
 //     array, or from the episode's record for an episode started inside the launch) in the
@@ -13,7 +13,7 @@
 //     register instead of the node id (lem layout below);
 //   * the step / counters / flags are two 32-bit words (the state's sc), not 8 registers;
 //   * the observed values (latency / cpu of every endpoint, zone capacities, dt, the request's
-//     topology row) live in a compact per-env LDS image (27 words) that a step updates in 5
+//     topology row) live in a compact per-env LDS image (40 words) that a step updates in 3
 //     words, and the copy-out decodes the float4 pieces from it straight into full-line
 //     stores (k_rollout_tpe built 18 float4 per env per step in registers and LDS);
 //   * the records of the envs that end inside the launch are drawn before the env state is
@@ -84,49 +84,91 @@ struct LDims {
     __device__ __forceinline__ LDims(const Params& p) : E(ET > 0 ? ET : p.E), R(ET > 0 ? RT : p.R) {}
 };
 
-// ---- k_rollout_img's per-env LDS image (IMG_W words, odd: conflict-free per-lane writes)
-//   [0] req_zone (f32)   [1] threshold (f32)   [2] dt (f32)
-//   [IMG_EP + 4e]: zone | zone_cpu_capacity << 2,  cpu (f32),  latency (f32),  topology
-//                  latency to the request's zone (f32)
-// The endpoint's first three words change only when it is selected (2 words) or an episode
-// starts; the request words and the topology column every step.  A float4 piece of the obs
-// rows is then 4 LDS words and no arithmetic but the zone / capacity conversion.
-constexpr int IMG_EP = 3, IMG_W = IMG_EP + 4 * TPE_E;  // 35
+// ---- k_rollout_img's per-env LDS image (IMG_W = 40 words, 16-byte row blocks)
+//   row block r at word 4r (r < E an endpoint; r = E the reject row, constant):
+//     [zc, topology, cpu, latency]   zc = the f16 pair (zone, zone cpu capacity) -- small
+//     integers (capacity <= 64 nodes x 8 cpus), exact in f16; the reject row's -1, -1 --
+//     then the endpoint's topology latency to the request's zone and its observed cpu and
+//     latency (f32)
+//   shared block at word IMG_S: [-, req_zone, threshold, dt] (f32)
+// Piece j of an env's obs (row j / 2, half j % 2) from its image:
+//   half 0 = (zone, capacity, cpu, topology) = (lo(zc), hi(zc), word 2, word 1) of row j / 2
+//   half 1 = (latency, req_zone, threshold, dt) = (word 3 of the row block, shared 1..3)
+// A store instruction of the copy-out covers 64 consecutive pieces of the wave's block and
+// P = 2R is even, so every lane stores the same half in every store (its lane parity): two
+// 16-byte LDS reads, the f16 pair's two conversions and four selects on a loop-invariant
+// flag per piece.  A step writes the selected endpoint's cpu + latency (one 8-byte write),
+// the shared block (one 16-byte write) and the topology column (E words).
+constexpr int IMG_S = 4 * (TPE_E + 1), IMG_W = IMG_S + 4;  // 36, 40
+constexpr uint32_t IMG_ZC_REJECT = 0xBC00BC00u;          // f16 pair (-1, -1)
+constexpr uint32_t F32_M1 = 0xBF800000u;                 // -1.f
+
+__device__ __forceinline__ uint32_t img_zc(int zone, int cap) {
+    const _Float16 z = (_Float16)zone, c = (_Float16)cap;
+    return (uint32_t)__builtin_bit_cast(uint16_t, z) | ((uint32_t)__builtin_bit_cast(uint16_t, c) << 16);
+}
 
 __device__ __forceinline__ void img_request(uint32_t* me, const LEnv& v, const uint32_t (&em)[TPE_E], int E) {
     const int rz = (int)((v.s1 >> S1_RZ) & 3);
     const float t0 = (float)topo_val(v.topo, 0, rz), t1 = (float)topo_val(v.topo, 1, rz);
     const float t2 = (float)topo_val(v.topo, 2, rz), t3 = (float)topo_val(v.topo, 3, rz);
-    me[0] = __float_as_uint((float)rz);
-    me[1] = __float_as_uint((float)threshold((int)((v.s1 >> S1_THR) & 7)));
-    me[2] = __float_as_uint(v.dt);
+    *reinterpret_cast<uint4*>(me + IMG_S) =
+        make_uint4(0u, __float_as_uint((float)rz), __float_as_uint((float)threshold((int)((v.s1 >> S1_THR) & 7))),
+                   __float_as_uint(v.dt));
 #pragma unroll
     for (int e = 0; e < TPE_E; ++e) {
         if (e >= E) continue;
         const int z = em_zone(em[e]);
         const float t = z == 0 ? t0 : (z == 1 ? t1 : (z == 2 ? t2 : t3));
-        me[IMG_EP + 4 * e + 3] = __float_as_uint(t);
+        me[4 * e + 1] = __float_as_uint(t);
     }
 }
-// piece j (row j / 2, half j % 2) of one env's rows from its image, without branches (the
-// lanes of one store hold both halves; the reject row's -1s are blended in bitwise)
-__device__ __forceinline__ float4 img_piece(const uint32_t* b, int j, int E) {
-    const int row = j >> 1;
-    const bool half = (j & 1) != 0, rej = row >= E;
-    const uint32_t* ep = b + IMG_EP + 4 * (rej ? 0 : row);
-    const uint32_t r0 = half ? ep[2] : ep[0];  // latency | zone word
-    const uint32_t r1 = half ? b[0] : ep[1];   // req_zone | cpu
-    const uint32_t r2 = half ? b[1] : ep[3];   // threshold | topology
-    const uint32_t r3 = b[2];                  // dt
-    const uint32_t x = half ? r0 : __float_as_uint((float)(r0 & 3));
-    const uint32_t y = half ? r1 : __float_as_uint((float)(r0 >> 2));
-    const uint32_t z = half ? r2 : r1;
-    const uint32_t w = half ? r3 : r2;
-    const uint32_t NEG = 0xBF800000u;                 // -1.f
-    const uint32_t mx = rej ? ~0u : 0u;               // reject row: x = -1
-    const uint32_t my = (rej && !half) ? ~0u : 0u;    // its first half: all -1
-    return make_float4(__uint_as_float((mx & NEG) | (~mx & x)), __uint_as_float((my & NEG) | (~my & y)),
-                       __uint_as_float((my & NEG) | (~my & z)), __uint_as_float((my & NEG) | (~my & w)));
+// the selected endpoint's new observed cpu and latency (words 2, 3 of its row block)
+__device__ __forceinline__ void img_sel(uint32_t* me, int e, float cpu, float lat) {
+    *reinterpret_cast<uint2*>(me + 4 * e + 2) = make_uint2(__float_as_uint(cpu), __float_as_uint(lat));
+}
+// piece of row block A / shared block S for a lane storing half h
+__device__ __forceinline__ float4 img_piece(const uint4& A, const uint4& S, bool h) {
+    const float zf = (float)__builtin_bit_cast(_Float16, (uint16_t)(A.x & 0xFFFFu));
+    const float cf = (float)__builtin_bit_cast(_Float16, (uint16_t)(A.x >> 16));
+    return make_float4(h ? __uint_as_float(A.w) : zf, h ? __uint_as_float(S.y) : cf,
+                       h ? __uint_as_float(S.z) : __uint_as_float(A.z), h ? __uint_as_float(S.w) : __uint_as_float(A.y));
+}
+
+// Copy-out cursor of a lane: the env (LDS byte offset ea of its image inside the wave's
+// image, index el) and row r2 of the lane's piece in the current store instruction.  One
+// store instruction further = 64 pieces = 32 rows further: r2 += 32 % R, el += 32 / R, and
+// one env more when r2 wraps.
+struct ImgCursor {
+    uint32_t ea;
+    int r2, el;
+};
+template <int ET, int RT>
+__device__ __forceinline__ ImgCursor img_cursor(const LDims<ET, RT>& d, int lane) {
+    int ln = lane;
+    // (opaque per call: the cursor of every store is a function of the lane only, and
+    // hoisting them out of the step loop would hold 2R of them in registers all launch)
+    asm volatile("" : "+v"(ln));
+    const int el = ln / (2 * d.R), r2 = (ln - el * 2 * d.R) >> 1;
+    return ImgCursor{(uint32_t)el * (uint32_t)(IMG_W * 4), r2, el};
+}
+template <int ET, int RT>
+__device__ __forceinline__ void img_advance(const LDims<ET, RT>& d, ImgCursor& c) {
+    const int dr = 32 % d.R, de = 32 / d.R;
+    c.r2 += dr;
+    c.ea += (uint32_t)(de * IMG_W * 4);
+    c.el += de;
+    if (c.r2 >= d.R) {
+        c.r2 -= d.R;
+        c.ea += IMG_W * 4;
+        c.el += 1;
+    }
+}
+__device__ __forceinline__ float4 img_read_piece(const uint32_t* wimg, const ImgCursor& c, bool h) {
+    const char* b = reinterpret_cast<const char*>(wimg) + c.ea;
+    const uint4 A = *reinterpret_cast<const uint4*>(b + 16 * c.r2);
+    const uint4 S = *reinterpret_cast<const uint4*>(b + 4 * IMG_S);
+    return img_piece(A, S, h);
 }
 
 // the next step's action (policy on the current state), its selected endpoint's 4 table
@@ -240,8 +282,7 @@ __device__ __forceinline__ double lean_apply(const Params& p, const LDims<ET, RT
             const uint32_t edo = e == oA ? (ed[e] & ~(0x3FFu << 20)) | ((uint32_t)Mn << 20) : ed[e];
             ed[e] = e == ai ? edA_new : edo;
         }
-        me[IMG_EP + 4 * ai + 1] = __float_as_uint((float)pr.next_cpu);
-        me[IMG_EP + 4 * ai + 2] = __float_as_uint((float)pr.next_lat);
+        img_sel(me, ai, (float)pr.next_cpu, (float)pr.next_lat);
         v.s1 &= ~(1u << S1_PEN);
         reward = accept_reward(p, pr.sel_lat, tl, pr.sel_cpu, v.acc2, (int)(v.s0 >> 16));
         v.last_r = reward;
@@ -270,16 +311,19 @@ __device__ __forceinline__ Scal lean_scal(const LEnv& v) {
 }
 
 // ---- k_rollout_img: the rollout with the env's observation rows kept as a compact LDS
-// image (IMG_W = 27 words per env) instead of registers + a per-step row image.
-// The step writes the words that changed (the selected endpoint's cpu and latency, dt and
-// the request words: 5 LDS writes instead of 18 16-byte ones), and the copy-out decodes
-// float4 pieces from the image straight into full-line stores of the wave's contiguous
-// obs block (a piece q of the wave: env q / 2R, piece q % 2R; 64 consecutive pieces per
-// store instruction).  Registers hold no observed values (olat / ocpu) and no row pieces,
-// LDS holds 6.9 KB per wave, so occupancy is set by the step state alone.
+// image (IMG_W = 40 words per env, above) instead of registers + a per-step row image.
+// The step writes what changed (the selected endpoint's cpu + latency, the shared request
+// block, the topology column), and the copy-out decodes float4 pieces from the image
+// straight into full-line stores of the wave's contiguous obs block (a piece q of the wave:
+// env q / 2R, piece q % 2R; 64 consecutive pieces per store instruction).  Registers hold
+// no observed values and no row pieces; LDS holds 10 KB per wave (4 blocks of 4 waves per
+// CU), so occupancy is set by the step state alone.  Round 3 replaced the 35-word image
+// whose pieces were decoded with 64-bit addressing and a division per store (~35 VALU per
+// piece) by the 16-byte row blocks and the per-lane cursor (~16): 1,680 -> 1,402 VALU per
+// wave-step (PMC), 2^20 staggered envs 80.2-81.6 -> 77.9-78.1 us per step at K = 20.
 
-// the env's endpoint words at an episode start (the zone capacity, the initial cpu and
-// latency = table rows 0)
+// the env's row blocks at the launch start (the observed values of the loaded state) and
+// the constant reject row
 template <int ET, int RT>
 __device__ __forceinline__ void img_endpoints(uint32_t* me, const LDims<ET, RT>& d, const uint32_t (&em)[TPE_E],
                                               uint64_t zcap, const float (&lat)[TPE_E], const float (&cpu)[TPE_E]) {
@@ -287,62 +331,37 @@ __device__ __forceinline__ void img_endpoints(uint32_t* me, const LDims<ET, RT>&
     for (int e = 0; e < TPE_E; ++e) {
         if (e >= d.E) continue;
         const int z = em_zone(em[e]);
-        me[IMG_EP + 4 * e] = (uint32_t)z | ((uint32_t)zcap_val(zcap, z) << 2);
-        me[IMG_EP + 4 * e + 1] = __float_as_uint(cpu[e]);
-        me[IMG_EP + 4 * e + 2] = __float_as_uint(lat[e]);
+        me[4 * e] = img_zc(z, zcap_val(zcap, z));
+        img_sel(me, e, cpu[e], lat[e]);
     }
+    *reinterpret_cast<uint4*>(me + 4 * d.E) = make_uint4(IMG_ZC_REJECT, F32_M1, F32_M1, F32_M1);
 }
 
-// the wave's rows from its image into out (the wave's block of 64 envs x P float4): store
-// instruction it covers pieces q = 64 it + lane, env q / P, piece q % P (PT = P when it is a
-// compile-time constant: the loop unrolls in pairs and the FLAGGED spans are constants).
-// FLAGGED = only the envs whose bit is set in m (their runs; stores holding none skipped).
-template <bool FLAGGED, int PT>
-__device__ __forceinline__ void img_copy_out(const uint32_t* wimg, float4* outw, int nenv, int P_, int E, int lane,
-                                             uint64_t m) {
-    const int P = PT > 0 ? PT : P_;
-    const int del = 64 / P, dj = 64 - del * P;
-    // (opaque per call: the pieces' LDS addresses depend on the lane only, and hoisting all 2R
-    // of them out of the step loop would hold them in registers across the whole launch)
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    int el = ln / P, j = ln - (ln / P) * P;
-#pragma unroll 1
-    for (int it = 0; it < P; ++it) {
-        bool go = el < nenv;
+// the wave's obs rows, store instructions [it0, it1) of the copy-out into out (the wave's
+// block of nenv envs x P float4: store it covers float4s 64 it .. 64 it + 63); c is the
+// lanes' cursor at it0 and is advanced past it1.  FLAGGED: only envs whose bit is set in m
+// (the terminal observations of the envs that finished).
+template <bool FLAGGED, int ET, int RT>
+__device__ __forceinline__ void img_copy(const LDims<ET, RT>& d, const uint32_t* wimg, float4* outw, int nenv,
+                                         int lane, ImgCursor& c, int it0, int it1, uint64_t m = 0) {
+    const bool h = (lane & 1) != 0;
+    const int P = 2 * d.R;
+    if (!FLAGGED && nenv == 64) {  // a full wave: every lane stores
+        for (int it = it0; it < it1; ++it) {
+            st_stream(at(outw + 64 * it, (uint32_t)lane * 16u), img_read_piece(wimg, c, h));
+            img_advance(d, c);
+        }
+        return;
+    }
+    for (int it = it0; it < it1; ++it) {
+        bool go = 64 * it + lane < nenv * P;
         if constexpr (FLAGGED) {
             const int lo = (64 * it) / P, hi = (64 * it + 63) / P;  // envs this store touches
             const uint64_t span = (hi >= 63 ? ~0ull : ((2ull << hi) - 1)) & ~((1ull << lo) - 1);
-            go = go && (m & span) && ((m >> el) & 1);
+            go = go && (m & span) && ((m >> c.el) & 1);
         }
-        if (go) st_stream(outw + 64 * it + lane, img_piece(wimg + el * IMG_W, j, E));
-        el += del;
-        j += dj;
-        if (j >= P) { j -= P; ++el; }
-    }
-}
-
-// The wave's obs stores [it0, it1) (store it = pieces 64 it .. 64 it + 63), branch-free: a
-// lane past the last live env (a partial last wave) repeats the last env's piece j, i.e. the
-// same value to the same address as the lane that owns it.  elj = the lane's (env, piece) at
-// it = 0 (el | j << 8).
-__device__ __forceinline__ void img_copy_range(const uint32_t* wimg, float4* outw, int nenv, int P, int E, int lane,
-                                               int elj, int it0, int it1) {
-    const int del = 64 / P, dj = 64 - del * P;
-    // (opaque per call: the pieces' LDS addresses depend on the lane only, and hoisting them
-    // out of the step loop would hold 2R of them in registers across the whole launch)
-    asm volatile("" : "+v"(elj));
-    int el = elj & 0xFF, j = elj >> 8;
-    // position at it0 (it0 * 64 pieces further)
-    const int q = 64 * it0 + el * P + j;
-    el = q / P;
-    j = q - el * P;
-    for (int it = it0; it < it1; ++it) {
-        const int ec = el < nenv ? el : nenv - 1;
-        st_stream(outw + (int64_t)ec * P + j, img_piece(wimg + ec * IMG_W, j, E));
-        el += del;
-        j += dj;
-        if (j >= P) { j -= P; ++el; }
+        if (go) st_stream(at(outw + 64 * it, (uint32_t)lane * 16u), img_read_piece(wimg, c, h));
+        img_advance(d, c);
     }
 }
 
@@ -368,9 +387,8 @@ __device__ __forceinline__ void img_start_episode(const Params& p, const LDims<E
             const double l0 = __longlong_as_double((long long)((uint64_t)lw[2 * i] | ((uint64_t)lw[2 * i + 1] << 32)));
             em[e] = lem_make(mw[i], l0);
             const int z = em_zone(mw[i]);
-            me[IMG_EP + 4 * e] = (uint32_t)z | ((uint32_t)zcap_val(zcap, z) << 2);
-            me[IMG_EP + 4 * e + 1] = __float_as_uint((float)em_c0(mw[i]));  // table rows 0: the initial values
-            me[IMG_EP + 4 * e + 2] = __float_as_uint((float)l0);
+            me[4 * e] = img_zc(z, zcap_val(zcap, z));
+            img_sel(me, e, (float)em_c0(mw[i]), (float)l0);  // table rows 0: the initial values
         }
     }
     (void)rw;
@@ -401,18 +419,18 @@ __device__ __forceinline__ void img_start_episode(const Params& p, const LDims<E
 template <int NB, int KIND, int ET, int RT, int MINW = 1>
 __global__ __launch_bounds__(NB, MINW) void k_rollout_img(Params p, int K, int32_t* act_out) {
     constexpr int NW = NB / 64;
-    __shared__ uint32_t simg[NW][64 * IMG_W];
+    __shared__ __attribute__((aligned(16))) uint32_t simg[NW][64 * IMG_W];
     const LDims<ET, RT> d(p);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t* wimg = simg[wv];
     uint32_t* me = wimg + lane * IMG_W;
-    const int64_t env0 = (int64_t)blockIdx.x * NB + (threadIdx.x & ~63);
+    // (the wave's first env, wave-uniform: its output blocks are scalar bases)
+    const int64_t env0 = (int64_t)blockIdx.x * NB + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63);
     const int64_t env = env0 + lane;
     const bool live = env < p.B;
     const int64_t ev = live ? env : 0;  // dead lanes step env 0's copy and store nothing
     const int E = d.E, R = d.R, P = 2 * R;
     const int nenv = p.B - env0 < 64 ? (int)(p.B - env0) : 64;
-    const int elj = (lane / (2 * R)) | ((lane % (2 * R)) << 8);  // the lane's first obs piece
 
     // first (with nothing else live), the next episodes of the envs that end inside the
     // launch, into their records (8 lanes per env); the list lives in the image region
@@ -509,7 +527,13 @@ __global__ __launch_bounds__(NB, MINW) void k_rollout_img(Params p, int K, int32
                                 v.total, v.sum_lat, v.sum_cpu, v.sum_hi);
             if (p.term_obs) {
                 wave_lds_sync();
-                img_copy_out<true, 2 * RT>(wimg, reinterpret_cast<float4*>(p.term_obs) + env0 * P, nenv, P, E, lane, m);
+                ImgCursor tc = img_cursor(d, lane);
+                // (an opaque scalar base: the stores' addresses are the same every step, and
+                // hoisting them out of the step loop would hold 2R address pairs all launch)
+                int64_t toff = env0 * P;
+                asm volatile("" : "+s"(toff));
+                float4* tob = reinterpret_cast<float4*>(p.term_obs) + toff;
+                img_copy<true>(d, wimg, tob, nenv, lane, tc, 0, P, m);
             }
             if (done) {
                 wave_lds_sync();  // (the copy-out read the terminal image)
@@ -523,11 +547,12 @@ __global__ __launch_bounds__(NB, MINW) void k_rollout_img(Params p, int K, int32
         // the stores of a wave spread over its step instead of one burst at the end
         float4* outw = p.obs ? reinterpret_cast<float4*>(p.obs + k * obs_slot) + env0 * P : nullptr;
         if (outw) wave_lds_sync();
+        ImgCursor cur = img_cursor(d, lane);
         auto stores = [&](int stage) {
             if (!outw) return;
             const int per = (P + PREP_STAGES - 1) / PREP_STAGES;
             const int it0 = stage * per, it1 = it0 + per < P ? it0 + per : P;
-            img_copy_range(wimg, outw, nenv, P, E, lane, elj, it0, it1);
+            img_copy<false>(d, wimg, outw, nenv, lane, cur, it0, it1);
         };
         if (k + 1 < K) {
             pr = lean_prep<KIND>(p, d, ev, v, em, ed, l0off, l0step, stores);
