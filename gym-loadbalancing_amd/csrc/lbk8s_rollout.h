@@ -512,6 +512,18 @@ __global__ __launch_bounds__(NB, MINW) void k_rollout_img(Params p, int K, int32
 #ifdef LB_TIMELINE
         if (g_timeline && lane == 0) g_timeline[gw * (K + 2) + 1 + k] = __builtin_amdgcn_s_memrealtime();
 #endif
+        // issue priority by progress: a wave behind the others in its launch goes first.
+        // (The default oldest-first lets the four waves of a block drift apart, and a block's
+        // LDS is released only when its slowest wave ends: 18-28% of the wave slots sat idle
+        // mid-launch, tools/timeline.py.)  2^20 staggered envs, K = 20: 77.7-78.0 -> 74.1-74.9
+        // us per step; K = 100 equal (profiles/r03_ablation.jsonl).
+        {
+            const int pl = 3 - (4 * k) / K;
+            if (pl >= 3) __builtin_amdgcn_s_setprio(3);
+            else if (pl == 2) __builtin_amdgcn_s_setprio(2);
+            else if (pl == 1) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         if (act_out && live) *at(act_out + (int64_t)k * p.B, envi * 4u) = pr.a;
         v.s0 += 1;  // step (<= L: the episode ends there)
         const bool done = live && (int)(v.s0 & 0xFFFF) == p.L;  // (:472)

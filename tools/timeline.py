@@ -71,6 +71,9 @@ def main():
                      "step_us_by_index": {int(i): round(float(sd[i]), 2) for i in pick},
                      "prologue_us": round(float(prolog[idx].mean()), 2)})
     res["generations"] = gens
+    # resident waves over time (20 us bins): the launch's ramp and drain
+    edges = np.arange(0.0, float(end.max()) + 20.0, 20.0)
+    res["active_waves_20us"] = [int(((start < e + 20.0) & (end > e)).sum()) for e in edges]
     print(json.dumps(res))
 
 
