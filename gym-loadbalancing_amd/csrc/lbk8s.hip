@@ -81,6 +81,48 @@ __global__ void k_replay_add(ReplayParams p) {
     }
 }
 
+// lb_replay_sample: SB3 ReplayBuffer.sample's (slot, env) draws and the gather; thread
+// (i, part): part < f4 -> obs float4, < 2 f4 -> next_obs float4, == 2 f4 -> the scalars
+struct ReplaySampleParams {
+    int64_t B;
+    int f4;
+    int64_t slots;
+    int batch;
+    uint64_t seed;
+    const int64_t* vstep;
+    const int64_t* base_adds;
+    const float4* rb_obs;
+    const float4* rb_next_obs;
+    const int64_t* rb_actions;
+    const float* rb_rewards;
+    const float* rb_dones;
+    float4* obs;
+    float4* next_obs;
+    int64_t* actions;
+    float* rewards;
+    float* dones;
+};
+__global__ void k_replay_sample(ReplaySampleParams p) {
+    const int parts = 2 * p.f4 + 1;
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= (int64_t)p.batch * parts) return;
+    const int i = (int)(q / parts), part = (int)(q - (int64_t)i * parts);
+    const int64_t t = *p.vstep, adds = *p.base_adds + t;
+    const int64_t upper = adds < p.slots ? (adds > 0 ? adds : 1) : p.slots;
+    const U4 w = philox((uint32_t)t, (uint32_t)((uint64_t)t >> 32), (uint32_t)i, D_DQN_SAMPLE, (uint32_t)p.seed,
+                        (uint32_t)(p.seed >> 32));
+    const int64_t bi = (int64_t)(((uint64_t)w.x * (uint64_t)upper) >> 32);  // upper < 2^32
+    const int64_t ei = (int64_t)bounded(w.y, (uint32_t)p.B);
+    const int64_t row = bi * p.B + ei;
+    if (part < p.f4) p.obs[(int64_t)i * p.f4 + part] = p.rb_obs[row * p.f4 + part];
+    else if (part < 2 * p.f4) p.next_obs[(int64_t)i * p.f4 + part - p.f4] = p.rb_next_obs[row * p.f4 + part - p.f4];
+    else {
+        p.actions[i] = p.rb_actions[row];
+        p.rewards[i] = p.rb_rewards[row];
+        p.dones[i] = p.rb_dones[row];
+    }
+}
+
 // lb_episode_log: VecMonitor's per-env float32 return and the finished episodes' rows,
 // appended to a device log (one atomic per wave: the ballot's count)
 struct EpLogParams {
@@ -749,19 +791,30 @@ unsigned ds_grid(int64_t groups) {
 
 template <int MODE>
 void ds_forward_launch(const DSParams& p, hipStream_t s) {
-    if constexpr (MODE != 1) {  // (the training forward covers R <= LB_DS_MAX_ELEMENTS)
-        if (p.R > LB_DS_MAX_ELEMENTS) {  // large sets: streamed in chunks, one env per wave
-            hipLaunchKernelGGL((k_deepsets_fwd_big<MODE>), dim3(ds_grid(p.B)), dim3(DS_BLOCK), 0, s, p);
-            return;
-        }
+    if (p.R > LB_DS_MAX_ELEMENTS) {  // large sets: streamed in chunks, one env per wave
+        hipLaunchKernelGGL((k_deepsets_fwd_big<MODE>), dim3(ds_grid(p.B)), dim3(DS_BLOCK), 0, s, p);
+        return;
     }
-    // a wave takes P envs per iteration: P = 4 for R <= 16, 2 for R <= 32, else 1
+    // a wave takes P envs per iteration: P = 4 for R <= 16, 2 for R <= 32, else 1 -- fewer
+    // when the batch would leave waves of the chip idle (the DQN vector step's 4096 envs:
+    // 1,024 groups of four filled 128 of the 256 CUs; its 128-set train step)
     const int ts = (p.R + 15) / 16;
-    const int P = ts == 1 ? 4 : (ts == 2 ? 2 : 1);
+    int P = ts == 1 ? 4 : (ts == 2 ? 2 : 1);
+    {
+        const int64_t waves = (int64_t)device_cus() * (DS_BLOCK / 64);
+        while (P > 1 && (p.B + P - 1) / P < waves) P /= 2;
+    }
     const unsigned grid = ds_grid((p.B + P - 1) / P);
     switch (ts) {
-        case 1: hipLaunchKernelGGL((k_deepsets_fwd<1, 4, MODE>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
-        case 2: hipLaunchKernelGGL((k_deepsets_fwd<2, 2, MODE>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
+        case 1:
+            if (P == 4) hipLaunchKernelGGL((k_deepsets_fwd<1, 4, MODE>), dim3(grid), dim3(DS_BLOCK), 0, s, p);
+            else if (P == 2) hipLaunchKernelGGL((k_deepsets_fwd<1, 2, MODE>), dim3(grid), dim3(DS_BLOCK), 0, s, p);
+            else hipLaunchKernelGGL((k_deepsets_fwd<1, 1, MODE>), dim3(grid), dim3(DS_BLOCK), 0, s, p);
+            break;
+        case 2:
+            if (P == 2) hipLaunchKernelGGL((k_deepsets_fwd<2, 2, MODE>), dim3(grid), dim3(DS_BLOCK), 0, s, p);
+            else hipLaunchKernelGGL((k_deepsets_fwd<2, 1, MODE>), dim3(grid), dim3(DS_BLOCK), 0, s, p);
+            break;
         case 3: hipLaunchKernelGGL((k_deepsets_fwd<3, 1, MODE>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
         case 4: hipLaunchKernelGGL((k_deepsets_fwd<4, 1, MODE>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
         default: hipLaunchKernelGGL((k_deepsets_fwd<5, 1, MODE>), dim3(grid), dim3(DS_BLOCK), 0, s, p); break;
@@ -813,12 +866,71 @@ int lb_replay_add(int64_t num_envs, int32_t obs_floats, int64_t slots, const int
     return check_launch();
 }
 
+int lb_dqn_act(const float* frag, const float* obs, int64_t num_envs, int32_t num_elements, const uint8_t* masks,
+               const void* state, const lb_config* cfg, const lb_dqn_explore* ex, int32_t* actions_out,
+               void* stream) {
+    if (int r = validate(cfg)) return r;
+    if (!frag || !obs || !state || !ex || !actions_out || num_envs < 1)
+        return fail("frag/obs/state/ex/actions_out NULL or num_envs < 1");
+    if (!ex->vstep_in || !ex->vstep_out || ex->vstep_in == ex->vstep_out || !ex->explore_out)
+        return fail("lb_dqn_explore: device words NULL (or vstep_in == vstep_out)");
+    if (cfg->rng_mode != LB_RNG_PHILOX) return fail("lb_dqn_act draws in Philox mode only");
+    const int32_t A = cfg->num_endpoints + (cfg->rejection_allowed ? 1 : 0);
+    if (num_elements != A) return fail("lb_dqn_act: num_elements must be the env's action count (R)");
+    if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS_FWD)
+        return fail("num_elements must be in [1, 257] (LB_DS_MAX_ELEMENTS_FWD)");
+    const Params e = make_params(const_cast<void*>(state), cfg, num_envs);
+    DSParams p{obs, frag, nullptr, nullptr, num_envs, num_elements, 1, 0, nullptr, nullptr, nullptr, nullptr,
+               actions_out, masks};
+    p.ex_on = 1;
+    p.ex = *ex;
+    p.ex_acc3 = e.acc3;
+    p.ex_sc = e.sc;
+    p.ex_env_offset = e.env_id_offset;
+    p.ex_key0 = e.key0;
+    p.ex_key1 = e.key1;
+    ds_forward_launch<2>(p, (hipStream_t)stream);
+    return check_launch();
+}
+
+int lb_dqn_head(const float* q, const float* q_next, const int64_t* actions, const float* rewards, const float* dones,
+                int64_t num_sets, int32_t num_elements, float gamma, float* dq_out, float* sq_err_out, float* td_out,
+                float* old_out, void* stream) {
+    if (!q || !q_next || !actions || !rewards || !dones || !dq_out || !sq_err_out || num_sets < 1)
+        return fail("lb_dqn_head: NULL buffer or num_sets < 1");
+    if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS_TRAIN) return fail("num_elements must be in [1, 257]");
+    DQNHeadParams p{q, q_next, actions, rewards, dones, num_sets, num_elements, gamma, 2.0f / (float)num_sets, dq_out,
+                    sq_err_out, td_out, old_out};
+    const unsigned grid = (unsigned)std::min<int64_t>((num_sets + 3) / 4, 65535);
+    hipLaunchKernelGGL(k_dqn_head, dim3(grid), dim3(256), 0, (hipStream_t)stream, p);
+    return check_launch();
+}
+
+int lb_replay_sample(int64_t num_envs, int32_t obs_floats, int64_t slots, int32_t batch, uint64_t seed,
+                     const int64_t* vstep, const int64_t* base_adds, const float* rb_obs, const float* rb_next_obs,
+                     const int64_t* rb_actions, const float* rb_rewards, const float* rb_dones, float* obs_out,
+                     float* next_obs_out, int64_t* actions_out, float* rewards_out, float* dones_out, void* stream) {
+    if (num_envs < 1 || obs_floats < 4 || obs_floats % 4 || slots < 1 || slots >= (1ll << 32) || batch < 1 ||
+        num_envs >= (1ll << 32))
+        return fail("bad replay sample geometry");
+    if (!vstep || !base_adds || !rb_obs || !rb_next_obs || !rb_actions || !rb_rewards || !rb_dones || !obs_out ||
+        !next_obs_out || !actions_out || !rewards_out || !dones_out)
+        return fail("replay sample buffers NULL");
+    ReplaySampleParams p{num_envs, obs_floats / 4, slots, batch, seed, vstep, base_adds,
+                         reinterpret_cast<const float4*>(rb_obs), reinterpret_cast<const float4*>(rb_next_obs),
+                         rb_actions, rb_rewards, rb_dones, reinterpret_cast<float4*>(obs_out),
+                         reinterpret_cast<float4*>(next_obs_out), actions_out, rewards_out, dones_out};
+    const int64_t n = (int64_t)batch * (2 * p.f4 + 1);
+    hipLaunchKernelGGL(k_replay_sample, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, p);
+    return check_launch();
+}
+
 int lb_ds_train_forward(const float* frag, const float* obs, int64_t num_envs, int32_t num_elements,
                         float* logits_out, float* psi_mean_out, float* save_actor, float* save_critic,
                         float* setvec_out, void* stream) {
     if (!frag || !obs || !setvec_out || num_envs < 1) return fail("frag/obs/setvec_out NULL or num_envs < 1");
-    if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS)
-        return fail("num_elements must be in [1, 80] (LB_DS_MAX_ELEMENTS)");
+    if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS_TRAIN)
+        return fail("num_elements must be in [1, 257] (LB_DS_MAX_ELEMENTS_TRAIN)");
     if (!logits_out && !psi_mean_out) return 0;
     if ((logits_out && !save_actor) || (psi_mean_out && !save_critic))
         return fail("a head's activation buffer is NULL");
@@ -835,7 +947,7 @@ int lb_ppo_head(const float* logits, const uint8_t* masks, const float* actions,
     if (!logits || !actions || !oldlogp || !adv || !ret || !vold || !value || !dlogits || !dvalue || !terms ||
         num_sets < 1)
         return fail("ppo head buffers NULL or num_sets < 1");
-    if (num_elements < 1 || num_elements > 128) return fail("num_elements must be in [1, 128]");
+    if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS_TRAIN) return fail("num_elements must be in [1, 257]");
     PPOHeadParams p{logits, masks, actions, oldlogp, adv, ret, vold, value, dlogits, dvalue, terms,
                     num_sets, num_elements, clip_coef, ent_coef, vf_coef, 1.0f / (float)num_sets, clip_vloss};
     const unsigned grid = (unsigned)std::min<int64_t>((num_sets + 3) / 4, 8192);
@@ -861,8 +973,8 @@ int lb_ds_train_backward(const float* bwd_frag, const float* obs, int64_t num_en
                   "weight-gradient layout and header disagree");
     if (!bwd_frag || !obs || !setvec || !wgrad_out || !workspace || num_envs < 1)
         return fail("bwd_frag/obs/setvec/wgrad_out/workspace NULL or num_envs < 1");
-    if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS)
-        return fail("num_elements must be in [1, 80] (LB_DS_MAX_ELEMENTS)");
+    if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS_TRAIN)
+        return fail("num_elements must be in [1, 257] (LB_DS_MAX_ELEMENTS_TRAIN)");
     const bool actor = dlogits != nullptr, critic = dmean != nullptr;
     if ((actor && !save_actor) || (critic && !save_critic)) return fail("a head's activation buffer is NULL");
     DSBwdParams p{obs, bwd_frag, save_actor, save_critic, dlogits, dmean, workspace, setvec,

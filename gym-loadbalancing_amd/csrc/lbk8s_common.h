@@ -40,7 +40,7 @@ constexpr int RO_REC_BYTES = 160; // k_rollout_tpe's next-episode record per env
 
 // Philox domains — the framework's draw map; restated by the oracle.
 enum : uint32_t { D_INIT = 1, D_NODE = 2, D_EP = 3, D_TOPO = 4, D_REQ_X = 5, D_REQ_I = 6,
-                  D_ACT = 7 };
+                  D_ACT = 7, D_DQN_EXPLORE = 8, D_DQN_SAMPLE = 9 };
 
 // ---- bit layouts -------------------------------------------------------------------
 // emeta (static per episode): zone[0:2) owner[2:10) type[10:13) c0[13:20) node[20:28)
@@ -222,9 +222,21 @@ __device__ __forceinline__ U4 draw(const Params& p, int64_t env, uint32_t episod
 
 // the env's uniform random action for this step (action_space.sample()): lb_policy's
 // LB_POLICY_RANDOM and lb_step's fused random policy (actions == NULL) draw the same value
+__device__ __forceinline__ int32_t random_action_raw(uint64_t gid, uint64_t acc3, uint32_t step, uint32_t key0,
+                                                     uint32_t key1, int A) {
+    const U4 w = philox((uint32_t)gid, (uint32_t)(acc3 >> 32), step, D_ACT | ((uint32_t)(gid >> 32) << 8), key0, key1);
+    return (int32_t)bounded(w.x, (uint32_t)A);
+}
 __device__ __forceinline__ int32_t random_action(const Params& p, int64_t env, uint64_t acc3, uint32_t step) {
-    const U4 w = draw(p, env, (uint32_t)(acc3 >> 32), step, D_ACT);
-    return (int32_t)bounded(w.x, (uint32_t)p.A);
+    return random_action_raw((uint64_t)(p.env_id_offset + env), acc3, step, p.key0, p.key1, p.A);
+}
+// the DQN's explore decision at vector step t (lb_dqn_act): eps = linear_schedule(t), one
+// uniform keyed by (seed, t) for every env
+__device__ __forceinline__ bool dqn_explores(const lb_dqn_explore& ex, int64_t t) {
+    const double eps = fmax(ex.slope * (double)t + ex.start_e, ex.end_e);  // linear_schedule (:32-34)
+    const U4 w = philox((uint32_t)t, (uint32_t)((uint64_t)t >> 32), 0u, D_DQN_EXPLORE, (uint32_t)ex.seed,
+                        (uint32_t)(ex.seed >> 32));
+    return u53(w.x, w.y) < eps;
 }
 
 template <bool TRACE>

@@ -23,6 +23,7 @@
 #include <cstdint>
 
 #include "lbk8s.h"
+#include "lbk8s_common.h"
 
 namespace lbk {
 
@@ -46,7 +47,31 @@ struct DSParams {
     // (masks[b][r] ? logits[b][r] : -1e8) (dqn_deepset.py:134-142); NULL = skip
     int32_t* actions;
     const uint8_t* masks;  // [B][R] or NULL (all valid)
+    // argmax mode, lb_dqn_act: the DQN's explore decision first (ex_on); exploring, every env
+    // takes its uniform random action (the env state's episode / step words) and no Q value
+    // is computed
+    int ex_on;
+    lb_dqn_explore ex;
+    const uint64_t* ex_acc3;
+    const uint64_t* ex_sc;
+    int64_t ex_env_offset;
+    uint32_t ex_key0, ex_key1;
 };
+
+// lb_dqn_act's decision: true when this launch explores (the random actions are written)
+__device__ __forceinline__ bool ds_dqn_explore(const DSParams& p) {
+    const int64_t t = *p.ex.vstep_in;
+    const bool explore = dqn_explores(p.ex, t);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *p.ex.explore_out = explore ? 1 : 0;
+        *p.ex.vstep_out = t + 1;
+    }
+    if (!explore) return false;
+    for (int64_t env = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; env < p.B; env += (int64_t)gridDim.x * blockDim.x)
+        p.actions[env] = random_action_raw((uint64_t)(p.ex_env_offset + env), p.ex_acc3[env],
+                                           (uint32_t)(p.ex_sc[env] & 0xFFFF), p.ex_key0, p.ex_key1, p.R);
+    return true;
+}
 
 // fragment layout of the packed weights (floats).  A matrix with KS input k-steps and NT
 // 16-row output tiles occupies NT*KS fragments of 64 floats; fragment (nt, k), lane l holds
@@ -217,9 +242,9 @@ __device__ __forceinline__ void set_max_store(const float (&h)[P * TS][KS], floa
             const int f0 = 16 * q + 4 * grp;
             *reinterpret_cast<float4*>(sv + off_max + f0) =
                 make_float4(M[(4 * q) * P + s], M[(4 * q + 1) * P + s], M[(4 * q + 2) * P + s], M[(4 * q + 3) * P + s]);
-            *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(sv + off_id) + f0) =
-                (uint32_t)(-m[(4 * q) * P + s]) | ((uint32_t)(-m[(4 * q + 1) * P + s]) << 8) |
-                ((uint32_t)(-m[(4 * q + 2) * P + s]) << 16) | ((uint32_t)(-m[(4 * q + 3) * P + s]) << 24);
+            *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(sv + off_id) + f0) =
+                make_uint2((uint32_t)(-m[(4 * q) * P + s]) | ((uint32_t)(-m[(4 * q + 1) * P + s]) << 16),
+                           (uint32_t)(-m[(4 * q + 2) * P + s]) | ((uint32_t)(-m[(4 * q + 3) * P + s]) << 16));
         }
     }
 }
@@ -277,6 +302,7 @@ __device__ __forceinline__ void store_rows(float* plane, const float (&h)[P * TS
 template <int TS, int P, int MODE>
 __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
     constexpr bool TRAIN = MODE == 1, ARGMAX = MODE == 2;
+    if (ARGMAX && p.ex_on && ds_dqn_explore(p)) return;  // (uniform: the DQN step explores)
     __shared__ __attribute__((aligned(16))) float W[DS_LDS_FLOATS];
     // stage the weight fragments (once per block; blocks are persistent); an actor-only
     // launch (DQN) stages only the actor's
@@ -476,10 +502,67 @@ __device__ __forceinline__ void load_obs_chunk(const float* x, int row0, int R, 
     }
 }
 
-// MODE 0: logits / value; 2: Q values and the masked greedy action (actor only)
+// training (chunked): each lane's running max of its rows per feature and the FIRST row
+// attaining it (strict > over ascending rows)
+template <int KS>
+__device__ __forceinline__ void chunk_argmax_acc(const float (&h)[DS_CT][KS], float (&v)[KS], float (&r)[KS], int row0,
+                                                 int col, int R) {
+#pragma unroll
+    for (int t = 0; t < DS_CT; ++t) {
+        const int row = row0 + 16 * t + col;
+        if (row >= R) continue;
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+            const bool u = h[t][k] > v[k];
+            v[k] = u ? h[t][k] : v[k];
+            r[k] = u ? (float)row : r[k];
+        }
+    }
+}
+// ... then the set's max over the 16 columns (into v, every lane) and the smallest row among
+// the lanes holding it, both to setvec (feature 16q + 4grp + i of the accumulator layout)
+__device__ __forceinline__ void chunk_argmax_store(float (&v)[16], float (&r)[16], int col, int grp, float* sv,
+                                                   int off_max, int off_id) {
+    float M[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) M[k] = v[k];
+    row_reduce<true>(M);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r[k] = v[k] == M[k] ? -r[k] : -1e9f;
+    row_reduce<true>(r);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = M[k];
+    if (col != 0) return;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int f0 = 16 * q + 4 * grp;
+        *reinterpret_cast<float4*>(sv + off_max + f0) = make_float4(M[4 * q], M[4 * q + 1], M[4 * q + 2], M[4 * q + 3]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(sv + off_id) + f0) =
+            make_uint2((uint32_t)(-r[4 * q]) | ((uint32_t)(-r[4 * q + 1]) << 16),
+                       (uint32_t)(-r[4 * q + 2]) | ((uint32_t)(-r[4 * q + 3]) << 16));
+    }
+}
+// a chunk's layer output rows (accumulator layout) into plane [B][R][64]
+__device__ __forceinline__ void store_rows_chunk(float* plane, const float (&h)[DS_CT][16], int64_t env, int R, int row0,
+                                                 int col, int grp) {
+#pragma unroll
+    for (int t = 0; t < DS_CT; ++t) {
+        const int row = row0 + 16 * t + col;
+        if (row >= R) continue;
+        float* q = plane + (env * (int64_t)R + row) * 64 + 4 * grp;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+            *reinterpret_cast<float4*>(q + 16 * nt) =
+                make_float4(h[t][4 * nt], h[t][4 * nt + 1], h[t][4 * nt + 2], h[t][4 * nt + 3]);
+    }
+}
+
+// MODE 0: logits / value; 1: training forward (activations, set maxima + first argmax rows,
+// psi mean; as k_deepsets_fwd<.., 1>); 2: Q values and the masked greedy action (actor only)
 template <int MODE>
 __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd_big(DSParams p) {
-    constexpr bool ARGMAX = MODE == 2;
+    constexpr bool ARGMAX = MODE == 2, TRAIN = MODE == 1;
+    if (ARGMAX && p.ex_on && ds_dqn_explore(p)) return;
     __shared__ __attribute__((aligned(16))) float W[DS_LDS_FLOATS];
     const int nstage = (ARGMAX || !p.critic) ? DS_C1L : DS_FLOATS;
     for (int i = threadIdx.x * 4; i < nstage; i += DS_BLOCK * 4)
@@ -504,19 +587,31 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd_big(DSParams p) {
             chunk_max_acc<2>(h0, m0, 16 * DS_CT * c, col, R);
         }
         row_reduce<true>(m0);
+        float* sv = TRAIN ? p.setvec + env * (int64_t)LB_DS_SETVEC_FLOATS : nullptr;
+        if (TRAIN && col == 0) {
+            sv[LB_DSV_MAX0 + grp] = m0[0];
+            sv[LB_DSV_MAX0 + 4 + grp] = m0[1];
+        }
         if (p.actor) {
-            float m1[16], m2[16];
+            float m1[16], m2[16], r1[16];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) m1[k] = m2[k] = -INFINITY;
+            for (int k = 0; k < 16; ++k) {
+                m1[k] = m2[k] = -INFINITY;
+                r1[k] = 1e9f;
+            }
             for (int c = 0; c < nch; ++c) {
                 uint32_t wo = 0;
                 asm volatile("" : "+s"(wo));
                 const float* Wc = W + wo;
                 load_obs_chunk(x, 16 * DS_CT * c, R, col, grp, h0);
                 eq_layer<DS_CT, 1, 2, 1>(Wc + DS_A1L, Wc + DS_A1G, h0, m0, h1, lane);
-                chunk_max_acc<16>(h1, m1, 16 * DS_CT * c, col, R);
+                if (TRAIN) chunk_argmax_acc<16>(h1, m1, r1, 16 * DS_CT * c, col, R);
+                else chunk_max_acc<16>(h1, m1, 16 * DS_CT * c, col, R);
             }
-            row_reduce<true>(m1);
+            if (TRAIN) chunk_argmax_store(m1, r1, col, grp, sv, LB_DSV_MAX1A, LB_DSV_ID1A);
+            else row_reduce<true>(m1);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) r1[k] = 1e9f;
             for (int c = 0; c < nch; ++c) {
                 uint32_t wo = 0;
                 asm volatile("" : "+s"(wo));
@@ -524,9 +619,11 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd_big(DSParams p) {
                 load_obs_chunk(x, 16 * DS_CT * c, R, col, grp, h0);
                 eq_layer<DS_CT, 1, 2, 1>(Wc + DS_A1L, Wc + DS_A1G, h0, m0, h1, lane);
                 eq_layer<DS_CT, 1, 16, 2>(Wc + DS_A2L, Wc + DS_A2G, h1, m1, h2, lane);
-                chunk_max_acc<16>(h2, m2, 16 * DS_CT * c, col, R);
+                if (TRAIN) chunk_argmax_acc<16>(h2, m2, r1, 16 * DS_CT * c, col, R);
+                else chunk_max_acc<16>(h2, m2, 16 * DS_CT * c, col, R);
             }
-            row_reduce<true>(m2);
+            if (TRAIN) chunk_argmax_store(m2, r1, col, grp, sv, LB_DSV_MAX2A, LB_DSV_ID2A);
+            else row_reduce<true>(m2);
             const float* G = W + DS_A3G + 16 * grp;
             float gl = 0.f;
 #pragma unroll
@@ -541,6 +638,10 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd_big(DSParams p) {
                 load_obs_chunk(x, 16 * DS_CT * c, R, col, grp, h0);
                 eq_layer<DS_CT, 1, 2, 1>(Wc + DS_A1L, Wc + DS_A1G, h0, m0, h1, lane);
                 eq_layer<DS_CT, 1, 16, 2>(Wc + DS_A2L, Wc + DS_A2G, h1, m1, h2, lane);
+                if (TRAIN) {
+                    store_rows_chunk(p.save_actor, h1, env, R, 16 * DS_CT * c, col, grp);
+                    store_rows_chunk(p.save_actor + p.B * (int64_t)R * 64, h2, env, R, 16 * DS_CT * c, col, grp);
+                }
 #pragma unroll
                 for (int t = 0; t < DS_CT; ++t) {
                     float v = 0.f;
@@ -570,11 +671,12 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd_big(DSParams p) {
         }
         if (ARGMAX || !p.critic) continue;
         // critic: the max of c1, then the max and the sum of c2, then layer 3 / rho as above
-        float mc1[16], mc2[16], sm[16];
+        float mc1[16], mc2[16], sm[16], rc[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             mc1[k] = mc2[k] = -INFINITY;
             sm[k] = 0.f;
+            rc[k] = 1e9f;
         }
         for (int c = 0; c < nch; ++c) {
             uint32_t wo = 0;
@@ -582,9 +684,13 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd_big(DSParams p) {
             const float* Wc = W + wo;
             load_obs_chunk(x, 16 * DS_CT * c, R, col, grp, h0);
             eq_layer<DS_CT, 1, 2, 2>(Wc + DS_C1L, Wc + DS_C1G, h0, m0, h1, lane);
-            chunk_max_acc<16>(h1, mc1, 16 * DS_CT * c, col, R);
+            if (TRAIN) chunk_argmax_acc<16>(h1, mc1, rc, 16 * DS_CT * c, col, R);
+            else chunk_max_acc<16>(h1, mc1, 16 * DS_CT * c, col, R);
         }
-        row_reduce<true>(mc1);
+        if (TRAIN) chunk_argmax_store(mc1, rc, col, grp, sv, LB_DSV_MAX1C, LB_DSV_ID1C);
+        else row_reduce<true>(mc1);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) rc[k] = 1e9f;
         for (int c = 0; c < nch; ++c) {
             uint32_t wo = 0;
             asm volatile("" : "+s"(wo));
@@ -592,14 +698,21 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd_big(DSParams p) {
             load_obs_chunk(x, 16 * DS_CT * c, R, col, grp, h0);
             eq_layer<DS_CT, 1, 2, 2>(Wc + DS_C1L, Wc + DS_C1G, h0, m0, h1, lane);
             eq_layer<DS_CT, 1, 16, 2>(Wc + DS_C2L, Wc + DS_C2G, h1, mc1, h2, lane);
-            chunk_max_acc<16>(h2, mc2, 16 * DS_CT * c, col, R);
+            if (TRAIN) {
+                chunk_argmax_acc<16>(h2, mc2, rc, 16 * DS_CT * c, col, R);
+                store_rows_chunk(p.save_critic, h1, env, R, 16 * DS_CT * c, col, grp);
+                store_rows_chunk(p.save_critic + p.B * (int64_t)R * 64, h2, env, R, 16 * DS_CT * c, col, grp);
+            } else {
+                chunk_max_acc<16>(h2, mc2, 16 * DS_CT * c, col, R);
+            }
 #pragma unroll
             for (int t = 0; t < DS_CT; ++t)
                 if (16 * DS_CT * c + 16 * t + col < R)
 #pragma unroll
                     for (int k = 0; k < 16; ++k) sm[k] += h2[t][k];
         }
-        row_reduce<true>(mc2);
+        if (TRAIN) chunk_argmax_store(mc2, rc, col, grp, sv, LB_DSV_MAX2C, LB_DSV_ID2C);
+        else row_reduce<true>(mc2);
         row_reduce<false>(sm);
         const float invR = 1.0f / (float)R;
         float mean[16];
@@ -612,6 +725,16 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd_big(DSParams p) {
             for (int k = 0; k < 16; ++k) acc = mfma4(W[DS_C3L + (nt * 16 + k) * 64 + lane], sm[k] * invR, acc);
 #pragma unroll
             for (int i = 0; i < 4; ++i) mean[4 * nt + i] = acc[i];
+        }
+        if (TRAIN) {  // psi mean (rho runs in torch): every column holds the set's value
+            if (col == 0) {
+                float* q = p.psi_mean + env * 64 + 4 * grp;
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt)
+                    *reinterpret_cast<float4*>(q + 16 * nt) =
+                        make_float4(mean[4 * nt], mean[4 * nt + 1], mean[4 * nt + 2], mean[4 * nt + 3]);
+            }
+            continue;
         }
         float r1[16];
 #pragma unroll

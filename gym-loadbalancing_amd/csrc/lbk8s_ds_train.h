@@ -50,18 +50,18 @@ enum : int {
     DSV_GS2C = 456,   //         sum_r dz2[r]
     DSV_MAX1C = 520,  //         max_set c1
     DSV_GS1C = 584,   //         sum_r dz1[r]
-    DSV_ID1A = 648,   // [64] u8: first argmax row of max_set h1 / h2 / c1 / c2 (forward)
-    DSV_ID2A = 664,
-    DSV_ID1C = 680,
-    DSV_ID2C = 696,
-    DSV_P1A = 712,    // actor: layer 1's pooled term per feature, V act'(MAX1) (k_ds_l1_pool)
-    DSV_P1C = 776,    // critic
-    DSV_FLOATS = 840,
+    DSV_ID1A = 648,   // [64] u16: first argmax row of max_set h1 / h2 / c1 / c2 (forward)
+    DSV_ID2A = 680,
+    DSV_ID1C = 712,
+    DSV_ID2C = 744,
+    DSV_P1A = 776,    // actor: layer 1's pooled term per feature, V act'(MAX1) (k_ds_l1_pool)
+    DSV_P1C = 840,    // critic
+    DSV_FLOATS = 904,
 };
 static_assert(DSV_MAX1A == LB_DSV_MAX1A && DSV_MAX2A == LB_DSV_MAX2A && DSV_MAX1C == LB_DSV_MAX1C &&
                   DSV_MAX2C == LB_DSV_MAX2C && DSV_ID1A == LB_DSV_ID1A && DSV_ID2A == LB_DSV_ID2A &&
                   DSV_ID1C == LB_DSV_ID1C && DSV_ID2C == LB_DSV_ID2C && DSV_P1A == LB_DSV_P1A && DSV_P1C == LB_DSV_P1C &&
-                  DSV_MAX0 == LB_DSV_MAX0,
+                  DSV_MAX0 == LB_DSV_MAX0 && DSV_FLOATS == LB_DS_SETVEC_FLOATS,
               "per-set vector layout and header disagree");
 
 constexpr int DSB_BLOCK = 512;                       // 8 waves: 2 per SIMD, one block per CU
@@ -133,9 +133,9 @@ struct Tile2 {
 };
 // a set's small inputs, loaded one set ahead
 struct SetIn {
-    float dl0, dl1;  // actor: dlogits of rows lane, lane + 64 (0 past R)
+    float dls;       // actor: this lane's share of sum_r dlogits (rows lane, lane + 64, ...)
     float dm;        // critic: dmean[lane]
-    int id2;         // ID2 bytes of features 4col .. 4col + 3
+    uint2 id2;       // ID2 rows (u16) of features 4col .. 4col + 3
     float4 mx2;      // MAX2 of features 4col .. 4col + 3
     float mx1;       // MAX1 of feature lane
 };
@@ -160,12 +160,14 @@ __device__ __forceinline__ void load_setin(const DSBwdParams& p, int64_t env, in
     const float* sv = p.setvec + env * (int64_t)DSV_FLOATS;
     if (HEAD == 0) {
         const float* dl = p.dlogits + env * (int64_t)R;
-        s.dl0 = lane < R ? dl[lane] : 0.f;
-        s.dl1 = lane + 64 < R ? dl[lane + 64] : 0.f;
+        float a = 0.f;  // (summed in row order per lane, then across the lanes)
+        for (int r = lane; r < R; r += 64) a += dl[r];
+        s.dls = a;
     } else {
         s.dm = p.dmean[env * 64 + lane];
     }
-    s.id2 = *reinterpret_cast<const int*>(reinterpret_cast<const uint8_t*>(sv + (HEAD == 0 ? DSV_ID2A : DSV_ID2C)) + 4 * col);
+    s.id2 = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(sv + (HEAD == 0 ? DSV_ID2A : DSV_ID2C)) +
+                                            4 * col);
     s.mx2 = *reinterpret_cast<const float4*>(sv + (HEAD == 0 ? DSV_MAX2A : DSV_MAX2C) + 4 * col);
     s.mx1 = sv[(HEAD == 0 ? DSV_MAX1A : DSV_MAX1C) + lane];
 }
@@ -241,7 +243,7 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
         auto env_of = [&](int64_t j) { return env0 + j * nwaves; };
         // per-set state (W layout: this lane's rows, features 4col .. 4col + 3)
         float S4[4], G4[4], gs1[4], g3 = 0.f;
-        int id2w = 0;
+        uint2 id2w = make_uint2(0u, 0u);
         float4 mx2v;
         float mx1l = 0.f;
 #pragma unroll
@@ -258,7 +260,7 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
             mx1l = cur.mx1;
             float c1, c2;
             if (HEAD == 0) {
-                float s = cur.dl0 + cur.dl1;
+                float s = cur.dls;
 #pragma unroll
                 for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
                 g3 = s;
@@ -344,7 +346,8 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
                     const float mn = fminf(y[m], 0.f);
-                    const float u = w * c1a[m] - (row == ((id2w >> (8 * m)) & 0xff) ? c2a[m] : 0.f);
+                    const uint32_t idw = m < 2 ? id2w.x : id2w.y;
+                    const float u = w * c1a[m] - (row == (int)((idw >> (16 * (m & 1))) & 0xffffu) ? c2a[m] : 0.f);
                     x[m] = u * mn + u;
                     S4[m] += w * mn;
                     G4[m] += w * y[m];  // actor: sum dl h2 (Lambda3); critic: sum c2
@@ -494,7 +497,7 @@ __global__ __launch_bounds__(64 * DSL_SUB) void k_ds_l1_pool(DSBwdParams p) {
     auto term = [&](int64_t s) {
         const float* sv = p.setvec + s * (int64_t)DSV_FLOATS;
         const float c = sv[(HEAD == 0 ? DSV_P1A : DSV_P1C) + o];
-        const int r = reinterpret_cast<const uint8_t*>(sv + (HEAD == 0 ? DSV_ID1A : DSV_ID1C))[o];
+        const int r = reinterpret_cast<const uint16_t*>(sv + (HEAD == 0 ? DSV_ID1A : DSV_ID1C))[o];
         const float4* x = reinterpret_cast<const float4*>(p.obs + (s * (int64_t)p.R + r) * 8);
         const float4 x0 = x[0], x1 = x[1];
         acc[0] += c * x0.x;
@@ -586,26 +589,43 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// rows lane + 64 j of a set, j < PH_J: R <= 64 PH_J (LB_DS_MAX_ELEMENTS_TRAIN = 257)
+constexpr int PH_J = 5;
 __global__ __launch_bounds__(256) void k_ppo_head(PPOHeadParams p) {
     const int lane = threadIdx.x & 63;
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
     const int R = p.R;
     for (int64_t s = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); s < p.M; s += nw) {
         const float* lg = p.logits + s * R;
-        const int r0 = lane, r1 = lane + 64;
-        const bool v0 = r0 < R, v1 = r1 < R;
-        const bool m0 = v0 && (!p.masks || p.masks[s * R + r0]);
-        const bool m1 = v1 && (!p.masks || p.masks[s * R + r1]);
-        const float l0 = v0 ? (m0 ? lg[r0] : -1e8f) : -INFINITY;
-        const float l1 = v1 ? (m1 ? lg[r1] : -1e8f) : -INFINITY;
-        const float mx = wave_max(fmaxf(l0, l1));
-        const float e0 = v0 ? expf(l0 - mx) : 0.f, e1 = v1 ? expf(l1 - mx) : 0.f;
-        const float lse = mx + logf(wave_sum(e0 + e1));
-        const float lp0 = l0 - lse, lp1 = l1 - lse;
-        const float p0 = v0 ? expf(lp0) : 0.f, p1 = v1 ? expf(lp1) : 0.f;
-        const float H = -wave_sum((v0 ? p0 * lp0 : 0.f) + (v1 ? p1 * lp1 : 0.f));
+        bool v[PH_J], m[PH_J];
+        float l[PH_J], lp[PH_J], pr[PH_J];
+        float lmax = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < PH_J; ++j) {
+            const int r = lane + 64 * j;
+            v[j] = r < R;
+            m[j] = v[j] && (!p.masks || p.masks[s * R + r]);
+            l[j] = v[j] ? (m[j] ? lg[r] : -1e8f) : -INFINITY;
+            lmax = fmaxf(lmax, l[j]);
+        }
+        const float mx = wave_max(lmax);
+        float es = 0.f;
+#pragma unroll
+        for (int j = 0; j < PH_J; ++j) es += v[j] ? expf(l[j] - mx) : 0.f;
+        const float lse = mx + logf(wave_sum(es));
+        float hs = 0.f;
+#pragma unroll
+        for (int j = 0; j < PH_J; ++j) {
+            lp[j] = l[j] - lse;
+            pr[j] = v[j] ? expf(lp[j]) : 0.f;
+            hs += v[j] ? pr[j] * lp[j] : 0.f;
+        }
+        const float H = -wave_sum(hs);
         const int a = (int)p.actions[s];
-        const float nlp = __shfl(a < 64 ? lp0 : lp1, a & 63);
+        float lpa = lp[0];
+#pragma unroll
+        for (int j = 1; j < PH_J; ++j) lpa = (a >> 6) == j ? lp[j] : lpa;
+        const float nlp = __shfl(lpa, a & 63);
         const float logratio = nlp - p.oldlogp[s];
         const float ratio = expf(logratio);
         const float A = p.adv[s];
@@ -616,8 +636,11 @@ __global__ __launch_bounds__(256) void k_ppo_head(PPOHeadParams p) {
         const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
         const float g_nlp = p.inv_m * (w1 * (-A) + (1.f - w1) * (-A) * inr) * ratio;
         const float ge = p.ent_coef * p.inv_m;
-        if (v0) p.dlogits[s * R + r0] = m0 ? g_nlp * ((r0 == a ? 1.f : 0.f) - p0) + ge * p0 * (lp0 + H) : 0.f;
-        if (v1) p.dlogits[s * R + r1] = m1 ? g_nlp * ((r1 == a ? 1.f : 0.f) - p1) + ge * p1 * (lp1 + H) : 0.f;
+#pragma unroll
+        for (int j = 0; j < PH_J; ++j) {
+            const int r = lane + 64 * j;
+            if (v[j]) p.dlogits[s * R + r] = m[j] ? g_nlp * ((r == a ? 1.f : 0.f) - pr[j]) + ge * pr[j] * (lp[j] + H) : 0.f;
+        }
         if (lane == 0) {
             const float v = p.value[s], rt = p.ret[s], vo = p.vold[s];
             const float vu = (v - rt) * (v - rt);
@@ -642,6 +665,46 @@ __global__ __launch_bounds__(256) void k_ppo_head(PPOHeadParams p) {
             t[3] = (ratio - 1.f) - logratio;
             t[4] = fabsf(ratio - 1.f) > p.clip ? 1.f : 0.f;
             t[5] = pgt - p.ent_coef * H + p.vf_coef * 0.5f * vt;
+        }
+    }
+}
+
+// DQN loss head (dqn_deepset.py:180-187) in one launch, one wave per sample:
+// td = r + gamma max_r q_next[r] (1 - done) (the target network's max; float32 in the
+// reference's operation order), old = q[a], sq_err = (td - old)^2 (F.mse_loss's terms), and
+// the loss's gradient w.r.t. q: 2 (old - td) / M at column a, 0 elsewhere (gather's backward).
+struct DQNHeadParams {
+    const float* q;       // [M][R] Q(obs) of the network being trained
+    const float* q_next;  // [M][R] the target network's Q(next_obs)
+    const int64_t* actions;
+    const float* rewards;
+    const float* dones;
+    int64_t M;
+    int R;
+    float gamma, two_over_m;
+    float* dq;      // [M][R]
+    float* sq_err;  // [M]
+    float* td;      // [M] or NULL
+    float* old;     // [M] or NULL
+};
+__global__ __launch_bounds__(256) void k_dqn_head(DQNHeadParams p) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
+    const int R = p.R;
+    for (int64_t s = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); s < p.M; s += nw) {
+        float m = -INFINITY;
+        for (int r = lane; r < R; r += 64) m = fmaxf(m, p.q_next[s * R + r]);
+        const float tmax = wave_max(m);
+        const float td = p.rewards[s] + p.gamma * tmax * (1.f - p.dones[s]);
+        const int a = (int)p.actions[s];
+        const float old = p.q[s * R + a];
+        const float d = td - old;
+        const float g = p.two_over_m * (old - td);
+        for (int r = lane; r < R; r += 64) p.dq[s * R + r] = r == a ? g : 0.f;
+        if (lane == 0) {
+            p.sq_err[s] = d * d;
+            if (p.td) p.td[s] = td;
+            if (p.old) p.old[s] = old;
         }
     }
 }

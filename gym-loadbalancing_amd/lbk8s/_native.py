@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblbk8s.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 LB_REWARD = {"naive": 0, "latency": 1, "fairness": 2, "multi": 3}
 LB_RNG_PHILOX, LB_RNG_TRACE = 0, 1
@@ -55,15 +55,23 @@ class LBDSWeightsC(C.Structure):
 
 
 LB_DS_FRAG_FLOATS = 33860
-LB_DS_MAX_ELEMENTS = 80       # training kernels
+LB_DS_MAX_ELEMENTS = 80       # forward held in registers (above: streamed in chunks)
+LB_DS_MAX_ELEMENTS_TRAIN = 257  # training forward / backward, PPO loss head
 LB_DS_MAX_ELEMENTS_FWD = 257  # inference forward / greedy argmax
 LB_DS_BWD_FLOATS = 24704
-LB_DS_SETVEC_FLOATS = 840
+LB_DS_SETVEC_FLOATS = 904
 LB_DS_WGRAD_FLOATS = 4608
 LB_DS_WORKSPACE_FLOATS = 1024 * 2 * LB_DS_WGRAD_FLOATS
 LB_DSV = {"MAX0": 0, "GA3": 8, "MAX2A": 72, "GS2A": 136, "MAX1A": 200, "GS1A": 264, "CS2": 328,
-          "MAX2C": 392, "GS2C": 456, "MAX1C": 520, "GS1C": 584, "ID1A": 648, "ID2A": 664, "ID1C": 680,
-          "ID2C": 696, "P1A": 712, "P1C": 776}
+          "MAX2C": 392, "GS2C": 456, "MAX1C": 520, "GS1C": 584, "ID1A": 648, "ID2A": 680, "ID1C": 712,
+          "ID2C": 744, "P1A": 776, "P1C": 840}
+
+
+class LBDQNExploreC(C.Structure):
+    """lb_dqn_explore (include/lbk8s.h)."""
+    _fields_ = [("start_e", C.c_double), ("slope", C.c_double), ("end_e", C.c_double), ("seed", C.c_uint64),
+                ("vstep_in", C.c_void_p), ("vstep_out", C.c_void_p), ("explore_out", C.c_void_p)]
+
 
 _lib = None
 
@@ -108,10 +116,14 @@ def lib():
     L.lb_ds_pack_backward.argtypes = [C.POINTER(LBDSWeightsC), vp, vp]
     L.lb_ds_train_backward.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp]
     L.lb_episode_log.argtypes = [i64, vp, vp, vp, vp, vp, vp, i64, vp, i64, vp, vp]
+    L.lb_dqn_act.argtypes = [vp, vp, i64, i32, vp, vp, cfgp, C.POINTER(LBDQNExploreC), vp, vp]
+    L.lb_dqn_head.argtypes = [vp, vp, vp, vp, vp, i64, i32, C.c_float, vp, vp, vp, vp, vp]
+    L.lb_replay_sample.argtypes = [i64, i32, i64, i32, C.c_uint64] + [vp] * 12 + [vp]
     for f in ("lb_validate_config", "lb_state_bytes", "lb_init", "lb_reset", "lb_step", "lb_policy", "lb_rollout",
               "lb_get_field", "lb_get_stats", "lb_status", "lb_ds_pack", "lb_ds_forward",
               "lb_ds_train_forward", "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax",
-              "lb_replay_add", "lb_ppo_head", "lb_episode_log"):
+              "lb_replay_add", "lb_ppo_head", "lb_episode_log", "lb_dqn_act", "lb_dqn_head",
+              "lb_replay_sample"):
         getattr(L, f).restype = C.c_int
     v = L.lb_abi_version()
     if v != ABI_VERSION:
@@ -134,4 +146,4 @@ EXPORTED_SYMBOLS = ("lb_abi_version", "lb_last_error", "lb_validate_config", "lb
                     "lb_init", "lb_reset", "lb_step", "lb_policy", "lb_rollout", "lb_get_field", "lb_get_stats",
                     "lb_status", "lb_ds_pack", "lb_ds_forward", "lb_ds_train_forward",
                     "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax", "lb_replay_add", "lb_ppo_head",
-                    "lb_episode_log")
+                    "lb_episode_log", "lb_dqn_act", "lb_dqn_head", "lb_replay_sample")

@@ -9,6 +9,14 @@ network's max (:180-186), MSE loss, Adam, hard target copy every
 target_network_frequency steps (tau = 1, :199-203).  total_timesteps counts VECTOR steps
 (:122).
 
+On a GPU the decisions the reference makes on the host are drawn by kernels (device RNG):
+the per-step explore draw random.random() < epsilon (:127) by lb_dqn_act, the replay
+sample (:177) by lb_replay_sample (Philox keyed by the learner seed and the vector step: the
+same distributions as the reference's generators, not their streams).  A train period --
+train_frequency vector steps and the train step -- then holds no host decision and replays
+as ONE HIP graph (period_graph=True, the default with train_graph); the eager run of the
+same kernels trains identically (tests/test_gpu_learners.py).
+
 Multi-GPU: gradients averaged with one all_reduce per train step (RCCL); every rank keeps
 its own envs and replay; the logged episode return is the mean over every rank's finished
 episodes (one 2-double all_reduce per log line).
@@ -23,7 +31,7 @@ import torch
 import torch.nn.functional as F
 from torch import optim
 
-from . import _native, fused
+from . import _native, fused, fused_train
 from . import dist as lbdist
 from .deepsets import DQNDeepSetAgent, HUGE_NEG, allreduce_gradients
 
@@ -113,7 +121,13 @@ class DeviceReplayBuffer:
 
 
 def dqn_loss(q_network, target_network, obs, actions, next_obs, rewards, dones, gamma):
-    """dqn_deepset.py:180-187 -> (loss, td_target, old_val)."""
+    """dqn_deepset.py:180-187 -> (loss, td_target, old_val).  With the fused kernels (a HIP
+    device) the TD target, the squared errors and the loss's gradient are one launch
+    (fused_train.dqn_head)."""
+    if fused.ENABLED and obs.is_cuda and fused_train.supported(q_network.q_network.net, obs):
+        with torch.no_grad():
+            q_next = fused.q_forward(target_network, next_obs)
+        return fused_train.dqn_head(q_network(obs), q_next, actions, rewards, dones, gamma)
     with torch.no_grad():
         target_max, _ = fused.q_forward(target_network, next_obs).max(dim=1)
         td_target = rewards.flatten() + gamma * target_max * (1 - dones.flatten())
@@ -126,7 +140,7 @@ class DQN_DeepSets:
                  buffer_size=10000, gamma=0.99, tau=1.0, n_minibatches: int = 4, target_network_frequency=500,
                  batch_size=128, start_e=1, end_e=0.05, exploration_fraction=0.5, learning_starts=10000,
                  train_frequency=10, device=None, log_fn=None, num_envs=None, tensorboard_log=None,
-                 train_graph=None):
+                 train_graph=None, period_graph=None, device_rng=None):
         # num_envs / tensorboard_log: accepted for signature compatibility with
         # dqn_deepset.py:46-67 (the env's num_envs is used; there is no tensorboard writer)
         self.env = env
@@ -181,6 +195,19 @@ class DQN_DeepSets:
         self._qfrag = fused.frag_buffer(self.device) if self.use_graphs else None
         self._obs = torch.zeros_like(self._next_obs)
         self._masks = torch.ones((self.num_envs, env.action_space.n), dtype=torch.bool, device=self.device)
+        # device RNG (GPU): explore decisions and replay samples drawn by kernels, keyed by
+        # this 64-bit seed and the vector step counter held in two alternating device words
+        self.device_rng = self.use_graphs and (True if device_rng is None else bool(device_rng))
+        self.period_graph = self.device_rng and self.train_graph and (True if period_graph is None
+                                                                      else bool(period_graph))
+        self._rng_seed = (int(seed) * 0x9E3779B97F4A7C15 + 0x632BE59BD9B4E019) & ((1 << 64) - 1)
+        self._vstep_pp = torch.zeros(2, dtype=torch.int64, device=self.device)
+        self._explore_flag = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._base_adds = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self._ex = [None, None]  # LBDQNExploreC per parity (kept alive: graphs hold their pointers' targets)
+        self._pgraphs = {}
+        self._pgraph_slope = None
+        self._tstatic = None
 
     def select_actions(self, obs, masks, epsilon):
         if random.random() < epsilon:  # one draw decides exploration for every env (:127)
@@ -217,6 +244,179 @@ class DQN_DeepSets:
         self.rb.add_device(obs, self._next_obs, self._act, self._rew, dones)
         obs.copy_(self._next_obs)
 
+    # ---- device-RNG mode -----------------------------------------------------------------
+    def _set_schedule(self, total_timesteps):
+        """lb_dqn_explore structs for this learn() call (linear_schedule's slope, :32-34)."""
+        from ._native import LBDQNExploreC
+        duration = self.exploration_fraction * total_timesteps
+        slope = (self.end_e - self.start_e) / duration
+        base = self._vstep_pp.data_ptr()
+        for parity in (0, 1):
+            self._ex[parity] = LBDQNExploreC(self.start_e, slope, self.end_e, self._rng_seed, base + 8 * parity,
+                                             base + 8 * (1 - parity), self._explore_flag.data_ptr())
+        return slope
+
+    def _vector_step_dev(self, obs, masks, parity):
+        """One vector step with the explore decision on the device: [random actions | greedy
+        actions from the packed image] in one launch (lb_dqn_act), the env step, lb_replay_add.
+        The q image (self._qfrag) is packed by the caller."""
+        env = self.env
+        env.dqn_act(self._qfrag, obs, masks, self._ex[parity], self._act)
+        env.step_device(self._act, obs_out=self._next_obs, reward_out=self._rew, done_out=self._done_u8)
+        self.rb.add_fused(obs, self._next_obs, self._act, self._rew, self._done_u8, env.ep_stats,
+                          self._ep_sum, self._ep_cnt, parity)
+
+    def _sample_dev(self, parity):
+        """lb_replay_sample into the train step's fixed buffers; the counter is the vector step
+        word of `parity` (the step count after the period's last step)."""
+        rb, B = self.rb, self.batch_size
+        if self._tstatic is None:
+            self._alloc_tstatic()
+        o, a, no, d, r = self._tstatic
+        vp = self._vstep_pp.data_ptr() + 8 * parity
+        _native.check(_native.lib().lb_replay_sample(
+            self.num_envs, int(rb.obs[0, 0].numel()), rb.size, B, self._rng_seed ^ 0x5851F42D4C957F2D, vp,
+            self._base_adds.data_ptr(), rb.obs.data_ptr(), rb.next_obs.data_ptr(), rb.actions.data_ptr(),
+            rb.rewards.data_ptr(), rb.dones.data_ptr(), o.data_ptr(), no.data_ptr(), a.data_ptr(), r.data_ptr(),
+            d.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream))
+
+    def _period_body(self, obs, masks, n, train, parity):
+        """n vector steps from `parity` then (train) the sample and the train step; returns
+        the graphs' split point for the all_reduce (multi-rank) via self._period_split."""
+        fused.pack_q_into(self.q_network, self._qfrag)
+        for i in range(n):
+            self._vector_step_dev(obs, masks, parity ^ (i & 1))
+        if train:
+            self._sample_dev(parity ^ (n & 1))
+            self._tloss = self._train_backward(*self._tstatic)
+
+    def _build_period_graphs(self, obs, masks):
+        """Capture the period graphs: keys (n, train, parity) for n in {1, train_frequency}."""
+        F = self.train_frequency
+        if self._tstatic is None:
+            self._alloc_tstatic()
+        # only the torch part needs a warm-up (its allocations); the vector steps and the
+        # sample are native launches on fixed buffers, captured without running them, so the
+        # env, the replay and the step counter are untouched and a graphed learn() follows
+        # the same trajectory as an eager one
+        self._train_warmup()
+        graphs = {}
+        keys = sorted({(1, False), (F, False), (F, True)})
+        for n, train in keys:
+            for parity in (0, 1):
+                self._tloss = None
+                ga = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(ga):
+                    self._period_body(obs, masks, n, train, parity)
+                    if train and not self._multi:
+                        self._train_apply()
+                gs = (ga,)
+                if train and self._multi:
+                    gb = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(gb):
+                        self._train_apply()
+                    gs = (ga, gb)
+                graphs[n, train, parity] = (gs, self._tloss)  # (each graph writes its own loss tensor)
+        return graphs
+
+    def _alloc_tstatic(self):
+        B, rb = self.batch_size, self.rb
+        obs_shape = tuple(rb.obs.shape[2:])
+        self._tstatic = (torch.zeros((B,) + obs_shape, device=self.device),
+                         torch.zeros((B, 1), dtype=torch.long, device=self.device),
+                         torch.zeros((B,) + obs_shape, device=self.device),
+                         torch.zeros((B, 1), device=self.device), torch.zeros((B, 1), device=self.device))
+
+    def _train_warmup(self):
+        """Two train steps on a side stream (grads, Adam state, workspaces allocated before a
+        capture), then the parameters and Adam state restored: nothing is drawn."""
+        params = list(self.q_network.parameters())
+        snap = [p.detach().clone() for p in params]
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                self._train_backward(*self._tstatic)
+                self._allreduce()
+                self._train_apply()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        with torch.no_grad():
+            for p, q in zip(params, snap):
+                p.copy_(q)
+            for st in self.optimizer.state.values():
+                for v in st.values():
+                    if isinstance(v, torch.Tensor):
+                        v.zero_()
+        fused.invalidate(self.q_network)
+
+    def _after_train(self, global_step):
+        fused.invalidate(self.q_network)
+        self.train_steps += 1
+        if global_step % self.target_network_frequency == 0:
+            with torch.no_grad():
+                for tp, qp in zip(self.target_network.parameters(), self.q_network.parameters()):
+                    tp.copy_(self.tau * qp + (1.0 - self.tau) * tp)
+            fused.invalidate(self.target_network)
+
+    def _learn_device(self, total_timesteps):
+        """learn() with device RNG: one graph replay per train period (period_graph) or the
+        same kernels eagerly."""
+        env = self.env
+        start = time.time()
+        obs, masks = self._obs, self._masks
+        slope = self._set_schedule(total_timesteps)
+        env.reset()
+        obs.copy_(env.obs)
+        if self.period_graph and (not self._pgraphs or self._pgraph_slope != slope):
+            # (captured, not run: the env, replay and counters are untouched)
+            self._pgraphs = self._build_period_graphs(obs, masks)
+            self._pgraph_slope = slope
+        self._parity = 0
+        self._vstep_pp.zero_()
+        self._base_adds.fill_(self.rb.size if self.rb.full else self.rb.pos)
+        F = self.train_frequency
+        loss = None
+        g = 0
+        while g < total_timesteps:
+            n = F if (g % F == 1 % F and g + F <= total_timesteps) else 1
+            last = g + n - 1
+            train = last > self.learning_starts and last % F == 0
+            if self.period_graph:
+                hit = self._pgraphs.get((n, train, self._parity))
+                if hit is None:  # (a step count the graphs do not hold)
+                    n, last = 1, g
+                    train = last > self.learning_starts and last % F == 0
+                    hit = self._pgraphs[n, train, self._parity]
+                gs, tloss = hit
+                gs[0].replay()
+                if len(gs) > 1:
+                    self._allreduce()  # eager collective on the current stream, between the two graphs
+                    gs[1].replay()
+                if train:
+                    loss = tloss
+            else:
+                self._period_body(obs, masks, n, train, self._parity)
+                if train:
+                    if self._multi and not self.train_graph:
+                        allreduce_gradients(self.q_network)
+                    else:
+                        self._allreduce()
+                    self._train_apply()
+                    loss = self._tloss
+            for _ in range(n):
+                self._parity ^= 1
+                self.rb.advance_host()
+            if train:
+                self._after_train(last)
+            if any(s % 1000 == 0 for s in range(g, last + 1)) or last == total_timesteps - 1:
+                eps = linear_schedule(self.start_e, self.end_e, self.exploration_fraction * total_timesteps, last)
+                self._flush_returns()
+                self.log_fn(dict(global_step=last, epsilon=eps, sps=(last + 1) / (time.time() - start),
+                                 loss=None if loss is None else loss.item(),
+                                 ep_return=self.episode_returns[-1] if self.episode_returns else float("nan")))
+            g = last + 1
+        return self
+
     def _build_graphs(self, obs, masks):
         """The four vector-step variants (explore or not, slot word 0 or 1) captured once as
         HIP graphs.  The warm-up steps run on a side stream before capture; the caller
@@ -242,7 +442,10 @@ class DQN_DeepSets:
         end packed in the flat bucket that the all_reduce averages."""
         loss, _, _ = dqn_loss(self.q_network, self.target_network, obs, actions, next_obs, rewards, dones,
                               self.gamma)
-        self.optimizer.zero_grad(set_to_none=not self.train_graph)
+        # (also inside a captured step: autograd then allocates the gradients from the graph's
+        # pool, at the same addresses every replay, and no zero fill + accumulate per parameter
+        # is recorded)
+        self.optimizer.zero_grad(set_to_none=True)
         loss.backward()
         if self._multi and self.train_graph:
             torch.cat([p.grad.reshape(-1) for p in self.q_network.parameters()], out=self._gflat)
@@ -335,6 +538,8 @@ class DQN_DeepSets:
 
     def learn(self, total_timesteps: int = 500000):
         env = self.env
+        if self.device_rng and not env.monitor:
+            return self._learn_device(total_timesteps)
         start = time.time()
         env.reset()
         obs, masks = self._obs, self._masks  # fixed buffers: the captured graphs use them

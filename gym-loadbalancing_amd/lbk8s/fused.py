@@ -145,6 +145,16 @@ def q_forward_graphable(qnet, x, out, frag):
     return out
 
 
+def pack_q_into(qnet, frag):
+    """Pack a DQNDeepSetAgent's live parameters into the fixed image `frag` (one launch;
+    graph-capturable: a replay re-packs the current parameters)."""
+    w, keep = _weights_struct(qnet.q_network.net, None)
+    _native.check(_native.lib().lb_ds_pack(C.byref(w), frag.data_ptr(),
+                                           torch.cuda.current_stream(frag.device).cuda_stream))
+    del keep
+    return frag
+
+
 @torch.no_grad()
 def q_argmax_graphable(qnet, x, masks, actions_out, frag, q_out=None):
     """Greedy actions of a DQNDeepSetAgent (dqn_deepset.py:134-142: argmax of the Q values

@@ -18,8 +18,9 @@ sets — runs in torch:
 
 The pooled gradient goes to the first row attaining the max, like torch.max in the
 reference's autograd; the forward kernel records each layer input's set-wise max and that
-row for the backward.  Covered geometry: 8 input features, 64 hidden, 1 <= R <= 80, on a
-HIP device; `supported()` says whether an input qualifies.
+row for the backward.  Covered geometry: 8 input features, 64 hidden, 1 <= R <= 257 (E <=
+256 and the reject row; above 80 the forward streams the set in 32-row chunks), on a HIP
+device; `supported()` says whether an input qualifies.
 """
 import ctypes as C
 
@@ -33,9 +34,10 @@ DSV = _native.LB_DSV
 
 
 def supported(actor_net, x) -> bool:
-    """The training kernels take R <= LB_DS_MAX_ELEMENTS (80); larger sets train through
-    the torch modules (with their GPU custom backward, deepsets._EquivariantFn)."""
-    return fused.ENABLED and fused._geometry_ok(actor_net, x) and x.shape[1] <= _native.LB_DS_MAX_ELEMENTS
+    """The training kernels take R <= LB_DS_MAX_ELEMENTS_TRAIN (257, the env's largest set);
+    anything else trains through the torch modules (with their GPU custom backward,
+    deepsets._EquivariantFn)."""
+    return fused.ENABLED and fused._geometry_ok(actor_net, x) and x.shape[1] <= _native.LB_DS_MAX_ELEMENTS_TRAIN
 
 
 def _stream(dev):
@@ -236,3 +238,39 @@ class _PPOHead(torch.autograd.Function):
 def ppo_head(logits, value, masks, actions, oldlogp, adv, ret, vold, clip_coef, ent_coef, vf_coef, clip_vloss):
     return _PPOHead.apply(logits, value, masks, actions, oldlogp, adv, ret, vold, clip_coef, ent_coef, vf_coef,
                           clip_vloss)
+
+
+class _DQNHead(torch.autograd.Function):
+    """dqn_deepset.py:180-187's loss from the trained network's Q values (lb_dqn_head): the
+    TD target from the target network's Q(next_obs) (no gradient), the squared errors and
+    their mean's gradient w.r.t. q, which backward returns (times the incoming gradient).
+    Returns (loss, td_target, old_val); the last two are not differentiable."""
+
+    @staticmethod
+    def forward(ctx, q, q_next, actions, rewards, dones, gamma):
+        M, R = q.shape
+        dev = q.device
+        q = q.float().contiguous()
+        dq = torch.empty_like(q)
+        sq = torch.empty((M,), dtype=torch.float32, device=dev)
+        td = torch.empty((M,), dtype=torch.float32, device=dev)
+        old = torch.empty((M,), dtype=torch.float32, device=dev)
+        keep = [q_next.float().contiguous(), actions.reshape(-1).to(torch.int64).contiguous(),
+                rewards.reshape(-1).float().contiguous(), dones.reshape(-1).float().contiguous()]
+        _native.check(_native.lib().lb_dqn_head(
+            q.data_ptr(), *[t.data_ptr() for t in keep], M, R, float(gamma), dq.data_ptr(), sq.data_ptr(),
+            td.data_ptr(), old.data_ptr(), _stream(dev)))
+        ctx.save_for_backward(dq)
+        ctx.mark_non_differentiable(td, old)
+        return sq.mean(), td, old
+
+    @staticmethod
+    def backward(ctx, gloss, gtd, gold):
+        (dq,) = ctx.saved_tensors
+        return dq * gloss, None, None, None, None, None
+
+
+def dqn_head(q, q_next, actions, rewards, dones, gamma):
+    """(F.mse_loss(td, q.gather(1, actions)), td, q.gather(1, actions)) with td = rewards +
+    gamma * q_next.max(1) * (1 - dones), and the loss's gradient, in one launch."""
+    return _DQNHead.apply(q, q_next, actions, rewards, dones, gamma)

@@ -201,7 +201,10 @@ class PPO_DeepSets:
         in the flat bucket that the all_reduce averages."""
         out = ppo_loss(self.agent, obs, actions, logprobs, masks, adv, ret, val,
                        self.clip_coef, self.ent_coef, self.vf_coef, self.norm_adv, self.clip_vloss)
-        self.optimizer.zero_grad(set_to_none=not self.use_graphs)
+        # (also inside a captured step: autograd then allocates the gradients from the graph's
+        # pool, at the same addresses every replay, and no zero fill + accumulate per parameter
+        # is recorded)
+        self.optimizer.zero_grad(set_to_none=True)
         out[0].backward()
         if self._multi:
             torch.cat([p.grad.reshape(-1) for p in self.agent.parameters()], out=self._gflat)

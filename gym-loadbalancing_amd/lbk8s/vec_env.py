@@ -461,6 +461,16 @@ class LBVecEnv:
                                         _native.LB_POLICY[kind], self._ptr(out), self._stream()))
         return out
 
+    def dqn_act(self, frag, obs, masks, ex, out):
+        """lb_dqn_act: the DQN's explore decision for this vector step drawn on the device (ex:
+        _native.LBDQNExploreC) and the actions into out -- every env's random action when
+        exploring, else the greedy action of the Q network packed in frag."""
+        R = obs.shape[1]
+        _native.check(self._L.lb_dqn_act(frag.data_ptr(), obs.data_ptr(), self.num_envs, R, self._ptr(masks),
+                                         self._ptr(self.state), C.byref(self._c), C.byref(ex), self._ptr(out),
+                                         self._stream()))
+        return out
+
     def field(self, name):
         """Env attribute as a float64 device tensor: (B, E) or (B,)."""
         shape = (self.num_envs,) if name in _native.PER_ENV_FIELDS else (self.num_envs, self.cfg.num_endpoints)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LBK8S_ABI_VERSION 5
+#define LBK8S_ABI_VERSION 6
 
 /* reward_function names of loadbalancer_k8s_env.py:20-31 */
 enum { LB_REWARD_NAIVE = 0, LB_REWARD_LATENCY = 1, LB_REWARD_FAIRNESS = 2, LB_REWARD_MULTI = 3 };
@@ -205,15 +205,16 @@ int lb_status(const void* state, const lb_config* cfg, int64_t num_envs, uint32_
  * the same equivariant stack, envs/deep_sets_agent_dqn.py:10-42).  Here one launch reads
  * an env's [R, 8] observation once and writes its R actor outputs and its critic value.
  * Only the reference geometry is supported: 8 input channels, 64 hidden.  Inference
- * (lb_ds_forward, lb_ds_q_argmax) takes R <= 257 (E <= 256 plus the reject row; above 80
- * the set is streamed through the kernel in 32-element chunks); the training entry points
- * take R <= 80.
+ * (lb_ds_forward, lb_ds_q_argmax) and training (lb_ds_train_*, lb_ppo_head) take R <= 257
+ * (E <= 256 plus the reject row; above 80 the forward streams the set through the kernel in
+ * 32-element chunks).
  * Weights are the torch parameters as they are (nn.Linear layout [out][in], f32, device);
  * lb_ds_pack rearranges them into the kernel's fragment order (LB_DS_FRAG_FLOATS floats),
  * to be redone after every optimizer step.  A NULL critic pointer set packs an actor-only
  * image (DQN); lb_ds_forward then must be called with value_out == NULL. */
 #define LB_DS_FRAG_FLOATS 33860
-#define LB_DS_MAX_ELEMENTS 80       /* training forward / backward */
+#define LB_DS_MAX_ELEMENTS 80       /* forward held in registers (above: streamed in chunks) */
+#define LB_DS_MAX_ELEMENTS_TRAIN 257 /* training forward / backward, PPO loss head */
 #define LB_DS_MAX_ELEMENTS_FWD 257  /* inference forward, greedy argmax */
 
 typedef struct lb_ds_weights {
@@ -252,6 +253,47 @@ int lb_replay_add(int64_t num_envs, int32_t obs_floats, int64_t slots, const int
                   int64_t* rb_actions, float* rb_rewards, float* rb_dones, double* ep_sum, double* ep_cnt,
                   void* stream);
 
+/* ---- DQN on the device (dqn_deepset.py:122-190): the explore decision and the replay
+ * sample drawn by the kernels, so a whole train period (train_frequency vector steps and
+ * the train step) replays as one HIP graph with no host decision inside it.
+ *
+ * lb_dqn_act: the vector step's actions in one launch.  eps = max(slope * t + start_e,
+ * end_e) (linear_schedule, :32-34) at t = *vstep_in; ONE uniform u (Philox keyed by seed,
+ * counter t) decides for every env, explore = u < eps (:127: random.random() < epsilon);
+ * writes *explore_out (0 / 1) and t + 1 to *vstep_out (a different word: callers alternate
+ * two).  Exploring, every env takes its uniform random action (lb_policy(LB_POLICY_RANDOM)'s
+ * draw from the env state; :128-131 with all-True masks); otherwise the greedy action of the
+ * Q network (lb_ds_q_argmax on frag / obs / masks, :134-142).  num_elements = the env's
+ * action count.  Replaces Python's random.random() stream by Philox (the distribution, not
+ * the stream, of the reference's decisions). */
+typedef struct lb_dqn_explore {
+    double start_e, slope, end_e; /* slope = (end_e - start_e) / duration (host float64) */
+    uint64_t seed;
+    const int64_t* vstep_in;      /* device */
+    int64_t* vstep_out;           /* device, != vstep_in */
+    int32_t* explore_out;         /* device [1] */
+} lb_dqn_explore;
+int lb_dqn_act(const float* frag, const float* obs, int64_t num_envs, int32_t num_elements, const uint8_t* masks,
+               const void* state, const lb_config* cfg, const lb_dqn_explore* ex, int32_t* actions_out,
+               void* stream);
+
+/* DQN loss head (dqn_deepset.py:180-187): per sample td = r + gamma max q_next (1 - done),
+ * sq_err_out = (td - q[a])^2 (mean = F.mse_loss) and dq_out = d mean / d q (2 (q[a] - td) /
+ * M at column a, 0 elsewhere); td_out / old_out (may be NULL) the TD target and q[a].
+ * q, q_next [M,R] f32; actions [M] int64; rewards, dones [M]. */
+int lb_dqn_head(const float* q, const float* q_next, const int64_t* actions, const float* rewards, const float* dones,
+                int64_t num_sets, int32_t num_elements, float gamma, float* dq_out, float* sq_err_out, float* td_out,
+                float* old_out, void* stream);
+
+/* Replay sample (SB3 ReplayBuffer.sample, :177): `batch` draws of (slot, env) uniform over
+ * slot < min(*base_adds + *vstep, slots) and env < num_envs (Philox keyed by seed, counter
+ * *vstep), gathered into obs_out / next_obs_out [batch, obs_floats], actions_out [batch]
+ * int64, rewards_out / dones_out [batch] f32, from the lb_replay_add layout. */
+int lb_replay_sample(int64_t num_envs, int32_t obs_floats, int64_t slots, int32_t batch, uint64_t seed,
+                     const int64_t* vstep, const int64_t* base_adds, const float* rb_obs, const float* rb_next_obs,
+                     const int64_t* rb_actions, const float* rb_rewards, const float* rb_dones, float* obs_out,
+                     float* next_obs_out, int64_t* actions_out, float* rewards_out, float* dones_out, void* stream);
+
 /* ---- Episode log (SB3 VecMonitor, run.py:122) -------------------------------------------
  * After a vector step: every env's float32 running return ret32[b] += reward[b] (VecMonitor
  * sums the float32 rewards, stable_baselines3 vec_monitor.py), and every env with done[b]
@@ -281,7 +323,7 @@ int lb_episode_log(int64_t num_envs, const uint8_t* done, const double* ep_stats
  *   critic dLambda3 = (dmean / R)^T CS2, dGamma3 = -dmean^T MAX2C.
  * The pooled gradient goes to the first row attaining the set-wise max (torch.max). */
 #define LB_DS_BWD_FLOATS 24704
-#define LB_DS_SETVEC_FLOATS 840
+#define LB_DS_SETVEC_FLOATS 904
 #define LB_DS_WGRAD_FLOATS 4608  /* per head: dLambda2 [64][64] then dLambda1 [64][8] */
 #define LB_DS_WORKSPACE_FLOATS (1024 * 2 * LB_DS_WGRAD_FLOATS)
 /* per-set vector offsets (floats) inside a LB_DS_SETVEC_FLOATS row */
@@ -296,12 +338,12 @@ int lb_episode_log(int64_t num_envs, const uint8_t* done, const double* ep_stats
 #define LB_DSV_GS2C 456
 #define LB_DSV_MAX1C 520
 #define LB_DSV_GS1C 584
-#define LB_DSV_ID1A 648  /* [64] u8 first argmax rows (16 floats of bytes) */
-#define LB_DSV_ID2A 664
-#define LB_DSV_ID1C 680
-#define LB_DSV_ID2C 696
-#define LB_DSV_P1A 712   /* [64] layer 1's pooled term per feature (actor) */
-#define LB_DSV_P1C 776   /* [64] (critic) */
+#define LB_DSV_ID1A 648  /* [64] u16 first argmax rows (32 floats of 16-bit rows) */
+#define LB_DSV_ID2A 680
+#define LB_DSV_ID1C 712
+#define LB_DSV_ID2C 744
+#define LB_DSV_P1A 776   /* [64] layer 1's pooled term per feature (actor) */
+#define LB_DSV_P1C 840   /* [64] (critic) */
 
 /* obs [B,R,8] -> logits_out [B,R] (actor; NULL = skip), psi_mean_out [B,64] (critic psi
  * averaged over the set; NULL = skip), save_actor [2,B,R,64] (h1 after ReLU, h2 after ELU),
@@ -312,7 +354,7 @@ int lb_ds_train_forward(const float* frag, const float* obs, int64_t num_envs, i
                         float* logits_out, float* psi_mean_out, float* save_actor, float* save_critic,
                         float* setvec_out, void* stream);
 
-/* PPO loss head (envs/ppo_deepset.py:227-263) for M sets of R <= 128 elements: per-set
+/* PPO loss head (envs/ppo_deepset.py:227-263) for M sets of R <= 257 elements: per-set
  * terms [M,6] (policy term max(pg1, pg2), value term, entropy, approx-kl term, clipped
  * indicator, loss term = pg - ent_coef H + vf_coef/2 v; their means are the reference's
  * logged scalars and loss) and the loss's gradient w.r.t. logits [M,R] and value [M],

@@ -95,6 +95,11 @@ int main() {
                       nullptr, nullptr, nullptr, nullptr) != 0);
     CHECK(lb_replay_add(1, 72, 4, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                         nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr) != 0);
+    CHECK(lb_dqn_act(nullptr, nullptr, 16, 9, nullptr, nullptr, &c, nullptr, nullptr, nullptr) != 0);
+    CHECK(lb_dqn_head(nullptr, nullptr, nullptr, nullptr, nullptr, 1, 9, 0.99f, nullptr, nullptr, nullptr, nullptr,
+                      nullptr) != 0);
+    CHECK(lb_replay_sample(1, 72, 4, 8, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                           nullptr, nullptr, nullptr, nullptr, nullptr) != 0);
     // out-of-range arguments past the NULL checks (fake, never-dereferenced pointers)
     void* fake = reinterpret_cast<void*>(0x1000);
     CHECK(lb_policy(fake, &c, 16, 9, (int32_t*)fake, nullptr) != 0);
@@ -103,7 +108,7 @@ int main() {
     CHECK(lb_ds_forward((const float*)fake, (const float*)fake, 1, 0, (float*)fake, nullptr, nullptr) != 0);
     CHECK(lb_ds_forward((const float*)fake, (const float*)fake, 1, LB_DS_MAX_ELEMENTS_FWD + 1, (float*)fake, nullptr,
                         nullptr) != 0);
-    CHECK(lb_ds_train_forward((const float*)fake, (const float*)fake, 1, LB_DS_MAX_ELEMENTS + 1, (float*)fake,
+    CHECK(lb_ds_train_forward((const float*)fake, (const float*)fake, 1, LB_DS_MAX_ELEMENTS_TRAIN + 1, (float*)fake,
                               nullptr, (float*)fake, nullptr, (float*)fake, nullptr) != 0);
     {
         lb_config t = base_cfg();

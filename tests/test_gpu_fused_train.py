@@ -57,7 +57,9 @@ def _check(got, exp, what, rtol, rel_floor):
 
 
 @pytest.mark.parametrize("R,ties", [(1, False), (7, True), (9, False), (9, True), (16, False), (17, True),
-                                    (33, False), (65, False), (65, True), (80, False)])
+                                    (33, False), (65, False), (65, True), (80, False),
+                                    # above 80: the chunked training forward; 257 = E 256 + reject row
+                                    (81, False), (129, True), (181, False), (257, True)])
 def test_train_step_matches_autograd(R, ties):
     from lbk8s import fused_train
     agent = _agent(200 + R)
@@ -122,7 +124,7 @@ def test_train_forward_caches_follow_updates():
         _check(p, q, f"param {name}", 1e-4, 1e-5)
 
 
-@pytest.mark.parametrize("R,masked", [(9, False), (65, True), (80, True)])
+@pytest.mark.parametrize("R,masked", [(9, False), (65, True), (80, True), (181, True), (257, False)])
 def test_ppo_head_matches_autograd(R, masked):
     """lb_ppo_head (loss terms and d loss / d logits, d loss / d value) against autograd
     through ppo_deepset.py:227-263's ops in float64 (the reference's formulation: masked

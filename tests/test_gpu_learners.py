@@ -43,10 +43,11 @@ def test_dqn_learns_end_to_end():
 
 
 def test_dqn_graph_train_step_matches_eager():
-    """The HIP-graph train step (captured once on fixed sample buffers, replayed) trains as
-    the eager one: same samples (the capture draws nothing), same updates; and after the
-    hard target syncs the fused forward of the target network sees the synced weights
-    (the cached weight image is rebuilt, not the initial one)."""
+    """One HIP graph per train period (train_frequency vector steps with the explore decisions
+    drawn on the device, the device replay sample and the train step; captured once,
+    replayed) trains as the same kernels run eagerly: same decisions, samples and updates;
+    and after the hard target syncs the fused forward of the target network sees the synced
+    weights (the cached weight image is rebuilt, not the initial one)."""
     from lbk8s import LBVecEnv, fused
     from lbk8s.dqn import DQN_DeepSets
     res = []
@@ -54,7 +55,7 @@ def test_dqn_graph_train_step_matches_eager():
         env = LBVecEnv(64, seed=4, as_tensors=True, episode_length=10)
         algo = DQN_DeepSets(env, buffer_size=64 * 100, batch_size=64, learning_starts=50, train_frequency=5,
                             target_network_frequency=100, seed=1, train_graph=graph)
-        assert algo.train_graph == graph
+        assert algo.train_graph == graph and algo.period_graph == graph and algo.device_rng
         algo.learn(total_timesteps=300)
         assert algo.train_steps == len([s for s in range(300) if s > 50 and s % 5 == 0])
         res.append([p.detach().clone() for p in algo.q_network.parameters()])
@@ -130,3 +131,110 @@ def test_ppo_config4_end_to_end_graph_step_matches_reference():
         close(p.grad / scale, d["grad__" + n.replace(".", "__")], what="grad " + n, rtol=1e-3,
               atol=max(2e-4, 1e-5 * gmax))
     check_adam_step(algo.agent, d, gmax, "cuda")
+
+
+def test_dqn_act_explore_decision():
+    """lb_dqn_act: eps = linear_schedule(t); one draw decides for every env; an exploring
+    step takes lb_policy(random)'s actions, a greedy one lb_ds_q_argmax's; the step counter
+    advances into the other word."""
+    from lbk8s import LBVecEnv, _native, fused
+    from lbk8s.dqn import DQN_DeepSets
+    env = LBVecEnv(256, seed=9, as_tensors=True, episode_length=10)
+    env.reset()
+    algo = DQN_DeepSets(env, seed=3)
+    frag = fused.frag_buffer(env.device)
+    fused.pack_q_into(algo.q_network, frag)
+    obs = env.obs.contiguous()
+    greedy = torch.empty(256, dtype=torch.int32, device="cuda")
+    fused.q_argmax_graphable(algo.q_network, obs, None, greedy, fused.frag_buffer(env.device))
+    pp = torch.zeros(2, dtype=torch.int64, device="cuda")
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    act = torch.full((256,), -7, dtype=torch.int32, device="cuda")
+
+    def ex(start, slope, end, parity=0):
+        b = pp.data_ptr()
+        return _native.LBDQNExploreC(start, slope, end, 1234, b + 8 * parity, b + 8 * (1 - parity), flag.data_ptr())
+    env.dqn_act(frag, obs, None, ex(1.0, 0.0, 1.0), act)  # always explore
+    assert int(flag.item()) == 1 and int(pp[1].item()) == 1
+    torch.testing.assert_close(act, env.policy("random"))
+    act.fill_(-7)
+    env.dqn_act(frag, obs, None, ex(0.0, 0.0, 0.0, parity=1), act)  # never
+    assert int(flag.item()) == 0 and int(pp[0].item()) == 2
+    torch.testing.assert_close(act, greedy)
+    # eps = 0.3: the decisions over 4000 steps explore ~30% of them
+    hits = 0
+    for t in range(4000):
+        pp[0] = t
+        env.dqn_act(frag, obs, None, ex(0.3, 0.0, 0.05), act)
+        hits += int(flag.item())
+    assert abs(hits / 4000 - 0.3) < 0.03
+    # the schedule's floor: slope * t + start below end_e gives end_e
+    n = 0
+    for t in range(2000):
+        pp[0] = 10 ** 6 + t
+        env.dqn_act(frag, obs, None, ex(1.0, -1.0, 0.5), act)
+        n += int(flag.item())
+    assert abs(n / 2000 - 0.5) < 0.04
+
+
+def test_dqn_head_matches_autograd():
+    """lb_dqn_head == F.mse_loss(r + gamma max q_next (1 - d), q.gather(1, a)) and its
+    gradient w.r.t. q (float64 autograd), at R = 9 and 257."""
+    import torch.nn.functional as F
+    from lbk8s import fused_train
+    g = torch.Generator().manual_seed(5)
+    for M, R in ((128, 9), (64, 257)):
+        q = torch.randn(M, R, generator=g)
+        qn = torch.randn(M, R, generator=g)
+        a = torch.randint(0, R, (M, 1), generator=g)
+        r = torch.randn(M, 1, generator=g)
+        d = (torch.rand(M, 1, generator=g) < 0.3).float()
+        qd = q.double().requires_grad_()
+        td = r.double().flatten() + 0.99 * qn.double().max(1)[0] * (1 - d.double().flatten())
+        ref = F.mse_loss(td, qd.gather(1, a).squeeze())
+        ref.backward()
+        qc = q.cuda().requires_grad_()
+        loss, tdc, oldc = fused_train.dqn_head(qc, qn.cuda(), a.cuda(), r.cuda(), d.cuda(), 0.99)
+        loss.backward()
+        torch.testing.assert_close(tdc.double().cpu(), td.detach(), rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(oldc.double().cpu(), qd.detach().gather(1, a).squeeze(), rtol=0, atol=0)
+        torch.testing.assert_close(loss.double().cpu(), ref.detach(), rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(qc.grad.double().cpu(), qd.grad, rtol=1e-5, atol=1e-7)
+
+
+def test_replay_sample_gathers_consistent_rows():
+    """lb_replay_sample: draws (slot, env) with slot < min(base_adds + vstep, slots) and
+    gathers the same (slot, env) row of every field."""
+    from lbk8s import _native
+    B, S, F, batch = 32, 10, 72, 512
+    dev = "cuda"
+    rid = (torch.arange(S, device=dev)[:, None] * 1000 + torch.arange(B, device=dev)[None, :]).float()  # (S, B)
+    rb_obs = rid[:, :, None].expand(S, B, F).contiguous()
+    rb_next = (rid + 0.5)[:, :, None].expand(S, B, F).contiguous()
+    rb_act = rid.long() + 7
+    rb_rew = rid + 0.25
+    rb_done = rid + 0.75
+    o = torch.empty((batch, F), device=dev)
+    no = torch.empty_like(o)
+    a = torch.empty(batch, dtype=torch.int64, device=dev)
+    r = torch.empty(batch, device=dev)
+    d = torch.empty(batch, device=dev)
+    vstep = torch.tensor([2], dtype=torch.int64, device=dev)
+    base = torch.tensor([1], dtype=torch.int64, device=dev)  # 3 slots filled
+    L = _native.lib()
+    _native.check(L.lb_replay_sample(B, F, S, batch, 99, vstep.data_ptr(), base.data_ptr(), rb_obs.data_ptr(),
+                                     rb_next.data_ptr(), rb_act.data_ptr(), rb_rew.data_ptr(), rb_done.data_ptr(),
+                                     o.data_ptr(), no.data_ptr(), a.data_ptr(), r.data_ptr(), d.data_ptr(), None))
+    torch.cuda.synchronize()
+    row = o[:, 0]
+    assert bool((o == row[:, None]).all()) and bool((no == (row + 0.5)[:, None]).all())
+    assert torch.equal(a, row.long() + 7) and torch.equal(r, row + 0.25) and torch.equal(d, row + 0.75)
+    slot, env = (row // 1000).long(), (row % 1000).long()
+    assert int(slot.max()) == 2 and int(slot.min()) == 0 and int(env.max()) == B - 1 and int(env.min()) == 0
+    # a full buffer: every slot reachable
+    base.fill_(100)
+    _native.check(L.lb_replay_sample(B, F, S, batch, 99, vstep.data_ptr(), base.data_ptr(), rb_obs.data_ptr(),
+                                     rb_next.data_ptr(), rb_act.data_ptr(), rb_rew.data_ptr(), rb_done.data_ptr(),
+                                     o.data_ptr(), no.data_ptr(), a.data_ptr(), r.data_ptr(), d.data_ptr(), None))
+    torch.cuda.synchronize()
+    assert int((o[:, 0] // 1000).max()) == S - 1

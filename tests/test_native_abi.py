@@ -48,7 +48,8 @@ def test_struct_offsets_match_compiled_header(tmp_path):
     import subprocess
 
     from lbk8s import _native
-    structs = {"lb_config": _native.LBConfigC, "lb_trace": _native.LBTraceC, "lb_ds_weights": _native.LBDSWeightsC}
+    structs = {"lb_config": _native.LBConfigC, "lb_trace": _native.LBTraceC, "lb_ds_weights": _native.LBDSWeightsC,
+               "lb_dqn_explore": _native.LBDQNExploreC}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "lbk8s.h"', "int main(void) {"]
     for cname, cls in structs.items():
         lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')

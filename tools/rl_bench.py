@@ -105,7 +105,9 @@ def main():
     else:
         from lbk8s.dqn import DQN_DeepSets
         dqn = DQN_DeepSets(env, seed=1, learning_starts=min(100, args.warmup // 2), device=dev,
-                           train_graph=os.environ.get("LBK8S_DQN_TRAIN_GRAPH", "1") == "1")  # (A/B switch)
+                           train_graph=os.environ.get("LBK8S_DQN_TRAIN_GRAPH", "1") == "1",  # (A/B switches)
+                           period_graph=os.environ.get("LBK8S_DQN_PERIOD_GRAPH", "1") == "1",
+                           device_rng=os.environ.get("LBK8S_DQN_DEVICE_RNG", "1") == "1")
         dqn.learn(args.warmup)
         barrier_sync()
         t0 = time.perf_counter()
@@ -117,6 +119,7 @@ def main():
                    unit="env-steps/s", vector_steps=args.steps, train_steps=dqn.train_steps,
                    ms_per_vector_step=wall / args.steps * 1e3,
                    buffer_slots_per_env=dqn.rb.size, train_graph=dqn.train_graph,
+                   period_graph=dqn.period_graph, device_rng=dqn.device_rng,
                    ep_return=dqn.episode_returns[-1] if dqn.episode_returns else None)
     if rank == 0:
         print(json.dumps(out), flush=True)
