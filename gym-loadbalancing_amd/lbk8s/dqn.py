@@ -208,6 +208,9 @@ class DQN_DeepSets:
         self._pgraphs = {}
         self._pgraph_slope = None
         self._tstatic = None
+        # the target network's image, packed when the target changes (every
+        # target_network_frequency steps), outside the captured periods
+        self._tfrag = fused.frag_buffer(self.device) if self.device_rng else None
 
     def select_actions(self, obs, masks, epsilon):
         if random.random() < epsilon:  # one draw decides exploration for every env (:127)
@@ -357,6 +360,7 @@ class DQN_DeepSets:
                 for tp, qp in zip(self.target_network.parameters(), self.q_network.parameters()):
                     tp.copy_(self.tau * qp + (1.0 - self.tau) * tp)
             fused.invalidate(self.target_network)
+            fused.pack_q_into(self.target_network, self._tfrag)
 
     def _learn_device(self, total_timesteps):
         """learn() with device RNG: one graph replay per train period (period_graph) or the
@@ -367,6 +371,24 @@ class DQN_DeepSets:
         slope = self._set_schedule(total_timesteps)
         env.reset()
         obs.copy_(env.obs)
+        # both images are pinned for the run: the q image is packed at the start of every
+        # period (the train step's forward reuses it: no repack inside the period), the
+        # target's when the target changes
+        fused.pack_q_into(self.q_network, self._qfrag)
+        fused.pack_q_into(self.target_network, self._tfrag)
+        fused.pin(self.q_network, self._qfrag)
+        fused.pin(self.target_network, self._tfrag)
+        try:
+            return self._learn_device_loop(total_timesteps, start, slope)
+        finally:
+            fused.pin(self.q_network, None)
+            fused.pin(self.target_network, None)
+            fused.invalidate(self.q_network)
+            fused.invalidate(self.target_network)
+
+    def _learn_device_loop(self, total_timesteps, start, slope):
+        env = self.env
+        obs, masks = self._obs, self._masks
         if self.period_graph and (not self._pgraphs or self._pgraph_slope != slope):
             # (captured, not run: the env, replay and counters are untouched)
             self._pgraphs = self._build_period_graphs(obs, masks)

@@ -60,15 +60,31 @@ def _geometry_ok(actor_net, x):
             and actor_net[0].Lambda.weight.shape == (64, 8) and actor_net[2].Lambda.weight.shape == (64, 64))
 
 
+_pinned = weakref.WeakKeyDictionary()
+
+
 def invalidate(module):
     """Drop `module`'s cached image: needed after parameter updates the version counters do
     not see (optimizer steps replayed from a HIP graph)."""
     _cache.pop(module, None)
 
 
+def pin(module, frag):
+    """Make `frag` (a fixed image the caller keeps current, e.g. packed at the start of a
+    captured DQN train period) the image of `module` for packed(): no pack is issued, in a
+    capture or not.  pin(module, None) undoes it."""
+    if frag is None:
+        _pinned.pop(module, None)
+    else:
+        _pinned[module] = frag
+
+
 def packed(module, actor_net, critic):
     """Fragment image of (actor_net, critic) cached on `module`; rebuilt after any update.
     While a HIP graph is being captured the pack is always issued (and so replayed)."""
+    pinned = _pinned.get(module)
+    if pinned is not None:
+        return pinned
     params = list(actor_net.parameters()) + (list(critic.parameters()) if critic is not None else [])
     version = tuple(p._version for p in params) + tuple(p.data_ptr() for p in params)
     hit = _cache.get(module)

@@ -71,18 +71,21 @@ def _vec(setvec, name, n=64):
 SET_CHUNK = 512  # sets per partial product of a reduction over the sets
 
 
-def _over_sets(a, b):
-    """a^T b for a (S, M), b (S, N): a reduction over S sets, split into chunk GEMMs plus a
-    sum so hipBLASLt gets ~S/512 independent tiles instead of one or two (a 51,200-long K
-    with a 64 x 64 output ran on two workgroups: 230 us; chunked: a few us)."""
+def _over_sets(a, b, alpha=1.0):
+    """alpha a^T b for a (S, M), b (S, N): a reduction over S sets, split into chunk GEMMs
+    plus a sum so hipBLASLt gets ~S/512 independent tiles instead of one or two (a
+    51,200-long K with a 64 x 64 output ran on two workgroups: 230 us; chunked: a few us).
+    alpha = -1 gives the Gamma gradients' sign in the GEMM itself (no negation kernel)."""
     S = a.shape[0]
     n = S // SET_CHUNK
+    z = a.new_empty(())  # (beta = 0: the input is ignored)
     if n < 2:
-        return a.t() @ b
+        return torch.addmm(z, a.t(), b, beta=0, alpha=alpha)
     m = n * SET_CHUNK
-    out = torch.bmm(a[:m].reshape(n, SET_CHUNK, -1).transpose(1, 2), b[:m].reshape(n, SET_CHUNK, -1)).sum(0)
+    out = torch.baddbmm(z, a[:m].reshape(n, SET_CHUNK, -1).transpose(1, 2), b[:m].reshape(n, SET_CHUNK, -1),
+                        beta=0, alpha=alpha).sum(0)
     if m < S:
-        out += a[m:].t() @ b[m:]
+        out.addmm_(a[m:].t(), b[m:], alpha=alpha)
     return out
 
 
@@ -135,20 +138,20 @@ class _FusedDeepSetsTrain(torch.autograd.Function):
         g3 = dlogits.sum(1)
         grads = [
             wgrad[0, 4096:].view(64, 8),                                       # actor Lambda1
-            -_over_sets(_vec(setvec, "GS1A"), max0),                           # actor Gamma1
+            _over_sets(_vec(setvec, "GS1A"), max0, -1.0),                      # actor Gamma1
             wgrad[0, :4096].view(64, 64),                                      # actor Lambda2
-            -_over_sets(_vec(setvec, "GS2A"), _vec(setvec, "MAX1A")),          # actor Gamma2
+            _over_sets(_vec(setvec, "GS2A"), _vec(setvec, "MAX1A"), -1.0),     # actor Gamma2
             _vec(setvec, "GA3").sum(0, keepdim=True),                          # actor Lambda3
-            -_over_sets(g3[:, None], _vec(setvec, "MAX2A")),                   # actor Gamma3
+            _over_sets(g3[:, None], _vec(setvec, "MAX2A"), -1.0),              # actor Gamma3
         ]
         if critic is not None:
             grads += [
                 wgrad[1, 4096:].view(64, 8),                                   # critic Lambda1
-                -_over_sets(_vec(setvec, "GS1C"), max0),                       # critic Gamma1
+                _over_sets(_vec(setvec, "GS1C"), max0, -1.0),                  # critic Gamma1
                 wgrad[1, :4096].view(64, 64),                                  # critic Lambda2
-                -_over_sets(_vec(setvec, "GS2C"), _vec(setvec, "MAX1C")),      # critic Gamma2
+                _over_sets(_vec(setvec, "GS2C"), _vec(setvec, "MAX1C"), -1.0), # critic Gamma2
                 _over_sets(dmean / R, _vec(setvec, "CS2")),                    # critic Lambda3
-                -_over_sets(dmean, _vec(setvec, "MAX2C")),                     # critic Gamma3
+                _over_sets(dmean, _vec(setvec, "MAX2C"), -1.0),                # critic Gamma3
             ]
         return (None, None, None, None) + tuple(grads)
 
