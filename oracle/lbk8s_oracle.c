@@ -102,7 +102,8 @@ static void philox4x32_r(uint32_t ctr[4], uint32_t k0, uint32_t k1, int rounds, 
 }
 
 /* domains of the framework's draw map */
-enum { D_INIT = 1, D_NODE = 2, D_EP = 3, D_TOPO = 4, D_REQ_X = 5, D_REQ_I = 6, D_ACT = 7 };
+enum { D_INIT = 1, D_NODE = 2, D_EP = 3, D_TOPO = 4, D_REQ_X = 5, D_REQ_I = 6, D_ACT = 7, D_DQN_EXPLORE = 8,
+       D_DQN_SAMPLE = 9 };
 
 static void draw(const orc_env* s, int64_t b, uint32_t episode, uint32_t slot, uint32_t dom,
                  uint32_t out[4]) {
@@ -557,6 +558,27 @@ void orc_philox_r(const uint32_t ctr[4], uint32_t k0, uint32_t k1, int32_t round
 }
 int32_t orc_philox_rounds(void) { return ORC_PHILOX_ROUNDS; }
 double orc_log(double x) { return fd_log(x); }
+
+/* The DQN's device decisions (include/lbk8s.h lb_dqn_act, lb_replay_sample), restated:
+ * dqn_deepset.py:125-127's epsilon-greedy draw at vector step t -- eps = linear_schedule
+ * (:32-34) = max(slope t + start_e, end_e), one u53 keyed by (seed, t) -- and SB3
+ * ReplayBuffer.sample's (slot, env) of sample i drawn at counter t. */
+int32_t orc_dqn_explore(uint64_t seed, double start_e, double slope, double end_e, int64_t t) {
+    const double a = slope * (double)t + start_e;
+    const double eps = a > end_e ? a : end_e;
+    uint32_t ctr[4] = {(uint32_t)t, (uint32_t)((uint64_t)t >> 32), 0u, D_DQN_EXPLORE}, w[4];
+    philox4x32_r(ctr, (uint32_t)seed, (uint32_t)(seed >> 32), ORC_PHILOX_ROUNDS, w);
+    return u53(w[0], w[1]) < eps ? 1 : 0;
+}
+void orc_replay_sample(uint64_t seed, int64_t t, int64_t upper, int64_t n_envs, int32_t batch, int64_t* slot,
+                       int64_t* env) {
+    for (int32_t i = 0; i < batch; ++i) {
+        uint32_t ctr[4] = {(uint32_t)t, (uint32_t)((uint64_t)t >> 32), (uint32_t)i, D_DQN_SAMPLE}, w[4];
+        philox4x32_r(ctr, (uint32_t)seed, (uint32_t)(seed >> 32), ORC_PHILOX_ROUNDS, w);
+        slot[i] = (int64_t)(((uint64_t)w[0] * (uint64_t)upper) >> 32);
+        env[i] = (int64_t)bounded(w[1], (uint32_t)n_envs);
+    }
+}
 
 /* Re-key the Philox stream (LBVecEnv.seed(): applied at the next full reset). */
 void orc_set_seed(void* h, uint64_t seed) { ((orc_env*)h)->c.seed = seed; }

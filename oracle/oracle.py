@@ -68,6 +68,10 @@ def lib():
         L.orc_log.restype = C.c_double
         L.orc_log.argtypes = [C.c_double]
         L.orc_set_seed.argtypes = [C.c_void_p, C.c_uint64]
+        L.orc_dqn_explore.restype = C.c_int32
+        L.orc_dqn_explore.argtypes = [C.c_uint64, C.c_double, C.c_double, C.c_double, C.c_int64]
+        L.orc_replay_sample.argtypes = [C.c_uint64, C.c_int64, C.c_int64, C.c_int64, C.c_int32, C.c_void_p,
+                                        C.c_void_p]
         _lib = L
     return _lib
 
@@ -245,6 +249,19 @@ def fd_log(x):
 
 def num_threads():
     return lib().orc_num_threads()
+
+
+def dqn_explore(seed, start_e, slope, end_e, t):
+    """The DQN's explore decision at vector step t (lb_dqn_act's draw)."""
+    return int(lib().orc_dqn_explore(int(seed), float(start_e), float(slope), float(end_e), int(t)))
+
+
+def replay_sample(seed, t, upper, n_envs, batch):
+    """(slot, env) int64 arrays of lb_replay_sample's draws at counter t."""
+    slot = np.zeros(batch, np.int64)
+    env = np.zeros(batch, np.int64)
+    lib().orc_replay_sample(int(seed), int(t), int(upper), int(n_envs), int(batch), _p(slot), _p(env))
+    return slot, env
 
 
 # ---- golden fixture helpers ---------------------------------------------------------------

@@ -1,6 +1,7 @@
 """GPU end-to-end runs of the device-resident learners (A16 PPO, A17 DQN) on LBVecEnv."""
 import math
 
+import numpy as np
 import pytest
 import torch
 
@@ -161,12 +162,16 @@ def test_dqn_act_explore_decision():
     env.dqn_act(frag, obs, None, ex(0.0, 0.0, 0.0, parity=1), act)  # never
     assert int(flag.item()) == 0 and int(pp[0].item()) == 2
     torch.testing.assert_close(act, greedy)
-    # eps = 0.3: the decisions over 4000 steps explore ~30% of them
+    # eps = 0.3: the decisions over 4000 steps explore ~30% of them, each one the C
+    # oracle's draw (oracle/lbk8s_oracle.c orc_dqn_explore, the same Philox map)
+    from oracle import oracle
     hits = 0
     for t in range(4000):
         pp[0] = t
         env.dqn_act(frag, obs, None, ex(0.3, 0.0, 0.05), act)
-        hits += int(flag.item())
+        f = int(flag.item())
+        assert f == oracle.dqn_explore(1234, 0.3, 0.0, 0.05, t), t
+        hits += f
     assert abs(hits / 4000 - 0.3) < 0.03
     # the schedule's floor: slope * t + start below end_e gives end_e
     n = 0
@@ -231,6 +236,10 @@ def test_replay_sample_gathers_consistent_rows():
     assert torch.equal(a, row.long() + 7) and torch.equal(r, row + 0.25) and torch.equal(d, row + 0.75)
     slot, env = (row // 1000).long(), (row % 1000).long()
     assert int(slot.max()) == 2 and int(slot.min()) == 0 and int(env.max()) == B - 1 and int(env.min()) == 0
+    # every (slot, env) is the C oracle's draw (orc_replay_sample)
+    from oracle import oracle
+    es, ee = oracle.replay_sample(99, 2, 3, B, batch)
+    assert np.array_equal(slot.cpu().numpy(), es) and np.array_equal(env.cpu().numpy(), ee)
     # a full buffer: every slot reachable
     base.fill_(100)
     _native.check(L.lb_replay_sample(B, F, S, batch, 99, vstep.data_ptr(), base.data_ptr(), rb_obs.data_ptr(),
