@@ -90,10 +90,11 @@ struct LDims {
 //     integers (capacity <= 64 nodes x 8 cpus), exact in f16; the reject row's -1, -1 --
 //     then the endpoint's topology latency to the request's zone and its observed cpu and
 //     latency (f32)
-//   shared block at word IMG_S: [-, req_zone, threshold, dt] (f32)
+//   shared block at word IMG_S: [req_zone, threshold, dt, -] (f32; 16-byte aligned, one
+//   12-byte LDS read)
 // Piece j of an env's obs (row j / 2, half j % 2) from its image:
 //   half 0 = (zone, capacity, cpu, topology) = (lo(zc), hi(zc), word 2, word 1) of row j / 2
-//   half 1 = (latency, req_zone, threshold, dt) = (word 3 of the row block, shared 1..3)
+//   half 1 = (latency, req_zone, threshold, dt) = (word 3 of the row block, shared 0..2)
 // A store instruction of the copy-out covers 64 consecutive pieces of the wave's block and
 // P = 2R is even, so every lane stores the same half in every store (its lane parity): two
 // 16-byte LDS reads, the f16 pair's two conversions and four selects on a loop-invariant
@@ -113,8 +114,8 @@ __device__ __forceinline__ void img_request(uint32_t* me, const LEnv& v, const u
     const float t0 = (float)topo_val(v.topo, 0, rz), t1 = (float)topo_val(v.topo, 1, rz);
     const float t2 = (float)topo_val(v.topo, 2, rz), t3 = (float)topo_val(v.topo, 3, rz);
     *reinterpret_cast<uint4*>(me + IMG_S) =
-        make_uint4(0u, __float_as_uint((float)rz), __float_as_uint((float)threshold((int)((v.s1 >> S1_THR) & 7))),
-                   __float_as_uint(v.dt));
+        make_uint4(__float_as_uint((float)rz), __float_as_uint((float)threshold((int)((v.s1 >> S1_THR) & 7))),
+                   __float_as_uint(v.dt), 0u);
 #pragma unroll
     for (int e = 0; e < TPE_E; ++e) {
         if (e >= E) continue;
@@ -131,8 +132,8 @@ __device__ __forceinline__ void img_sel(uint32_t* me, int e, float cpu, float la
 __device__ __forceinline__ float4 img_piece(const uint4& A, const uint4& S, bool h) {
     const float zf = (float)__builtin_bit_cast(_Float16, (uint16_t)(A.x & 0xFFFFu));
     const float cf = (float)__builtin_bit_cast(_Float16, (uint16_t)(A.x >> 16));
-    return make_float4(h ? __uint_as_float(A.w) : zf, h ? __uint_as_float(S.y) : cf,
-                       h ? __uint_as_float(S.z) : __uint_as_float(A.z), h ? __uint_as_float(S.w) : __uint_as_float(A.y));
+    return make_float4(h ? __uint_as_float(A.w) : zf, h ? __uint_as_float(S.x) : cf,
+                       h ? __uint_as_float(S.y) : __uint_as_float(A.z), h ? __uint_as_float(S.z) : __uint_as_float(A.y));
 }
 
 // Copy-out cursor of a lane: the env (LDS byte offset ea of its image inside the wave's
