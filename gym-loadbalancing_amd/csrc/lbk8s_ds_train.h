@@ -147,8 +147,11 @@ __device__ __forceinline__ void load_tile2(const DSBwdParams& p, const float* in
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const int64_t er = env * (int64_t)R + min(16 * t + 4 * c + grp, R - 1);
-        s.a[c] = *reinterpret_cast<const float4*>(in2 + er * 64 + 4 * col);
-        s.h[c] = *reinterpret_cast<const float4*>(in1 + er * 64 + 4 * col);
+        // (the activations are read once: nontemporal loads keep them out of the caches)
+        const dsf4 a4 = __builtin_nontemporal_load(reinterpret_cast<const dsf4*>(in2 + er * 64 + 4 * col));
+        const dsf4 h4 = __builtin_nontemporal_load(reinterpret_cast<const dsf4*>(in1 + er * 64 + 4 * col));
+        s.a[c] = make_float4(a4[0], a4[1], a4[2], a4[3]);
+        s.h[c] = make_float4(h4[0], h4[1], h4[2], h4[3]);
         s.x[c] = p.obs[er * 8 + (col & 7)];
         s.d[c] = HEAD == 0 ? p.dlogits[er] : 0.f;
     }
