@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Experiment check: lb_rollout under rollout variant V (default 11, the persistent
+k_rollout_img) against the product dispatch (variant 0) on two identically seeded,
+staggered env batches: obs, reward, done, actions, terminal obs, episode stats and the
+env state words after three launches must be bit-identical.
+
+    python tools/persist_check.py [--envs 300001] [--K 20] [--variant 11]
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "gym-loadbalancing_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=300001)
+    ap.add_argument("--K", type=int, default=20)
+    ap.add_argument("--variant", type=int, default=11)
+    args = ap.parse_args()
+    import torch
+
+    from lbk8s import LBVecEnv, _native
+    L = _native.lib()
+    L.lbx_set_rollout_variant.argtypes = [C.c_int]
+    dev = torch.device("cuda", 0)
+    B, K = args.envs, args.K
+    outs = []
+    for var in (0, args.variant):
+        L.lbx_set_rollout_variant(0)
+        env = LBVecEnv(B, device=dev, seed=5, as_tensors=True)
+        R, EL = env.cfg.obs_rows, env.cfg.episode_length
+        env.reset()
+        gid = torch.arange(B, device=dev)
+        tmp = torch.empty((B, R, 8), device=dev)
+        for r in range(1, EL):
+            env.step_device(None, obs_out=tmp)
+            env.reset_masked((gid % EL) == r)
+        L.lbx_set_rollout_variant(var)
+        res = []
+        for _ in range(3):
+            obs = torch.empty((K, B, R, 8), device=dev)
+            rew = torch.empty((K, B), device=dev)
+            done = torch.empty((K, B), dtype=torch.uint8, device=dev)
+            act = torch.empty((K, B), dtype=torch.int32, device=dev)
+            env.rollout("random", K, obs_out=obs, reward_out=rew, done_out=done, actions_out=act)
+            res += [obs, rew, done, act, env.terminal_obs.clone(), env.ep_stats.clone()]
+        torch.cuda.synchronize()
+        res.append(env.state.clone())
+        L.lbx_set_rollout_variant(0)
+        assert env.status() == 0
+        outs.append(res)
+    bad = [i for i, (a, b) in enumerate(zip(*outs)) if not torch.equal(a, b)]
+    print({"envs": B, "K": K, "variant": args.variant, "tensors": len(outs[0]), "mismatch": bad})
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    main()
