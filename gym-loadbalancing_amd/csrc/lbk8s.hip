@@ -1000,4 +1000,36 @@ int lb_ds_train_backward(const float* bwd_frag, const float* obs, int64_t num_en
     return check_launch();
 }
 
+int lb_ds_set_grads(const float* setvec, const float* dlogits, const float* dmean, int64_t num_sets,
+                    int32_t num_elements, float* out, void* stream) {
+    if (!setvec || !dlogits || !out || num_sets < 1) return fail("setvec/dlogits/out NULL or num_sets < 1");
+    if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS_TRAIN)
+        return fail("num_elements must be in [1, 257] (LB_DS_MAX_ELEMENTS_TRAIN)");
+    const int SV = LB_DS_SETVEC_FLOATS;
+    SetGradParams p{};
+    p.S = num_sets;
+    int nj = 0;
+    auto job = [&](const float* a, int lda, int M, int amode, int alen, int boff, const float* b, int ldb, int N,
+                   float scale, float* o) {
+        p.job[nj++] = SetGradJob{a, lda, M, amode, alen, b ? b : setvec + boff, ldb, N, scale, o};
+    };
+    // actor: dGamma1 = -GS1A^T MAX0, dGamma2 = -GS2A^T MAX1A, dLambda3 = sum GA3,
+    // dGamma3 = -(row sums of dlogits)^T MAX2A
+    job(setvec + LB_DSV_GS1A, SV, 64, 0, 0, LB_DSV_MAX0, nullptr, SV, 8, -1.f, out);
+    job(setvec + LB_DSV_GS2A, SV, 64, 0, 0, LB_DSV_MAX1A, nullptr, SV, 64, -1.f, out + 512);
+    job(nullptr, 0, 1, 1, 0, LB_DSV_GA3, nullptr, SV, 64, 1.f, out + 4608);
+    job(dlogits, num_elements, 1, 2, num_elements, LB_DSV_MAX2A, nullptr, SV, 64, -1.f, out + 4672);
+    if (dmean) {  // critic: the same for psi, layer 3 from dmean (the mean's 1/R on Lambda3)
+        float* c = out + LB_DS_SETGRAD_ACTOR;
+        job(setvec + LB_DSV_GS1C, SV, 64, 0, 0, LB_DSV_MAX0, nullptr, SV, 8, -1.f, c);
+        job(setvec + LB_DSV_GS2C, SV, 64, 0, 0, LB_DSV_MAX1C, nullptr, SV, 64, -1.f, c + 512);
+        job(dmean, 64, 64, 0, 0, LB_DSV_CS2, nullptr, SV, 64, 1.f / (float)num_elements, c + 4608);
+        job(dmean, 64, 64, 0, 0, LB_DSV_MAX2C, nullptr, SV, 64, -1.f, c + 8704);
+    }
+    static_assert(LB_DS_SETGRAD_ACTOR == 4736 && LB_DS_SETGRAD_CRITIC == 12800, "set-gradient layout");
+    hipLaunchKernelGGL(k_ds_set_grads, dim3((64 * 64 + SG_THREADS - 1) / SG_THREADS, nj), dim3(SG_THREADS), 0,
+                       (hipStream_t)stream, p);
+    return check_launch();
+}
+
 }  // extern "C"

@@ -734,4 +734,72 @@ __global__ void k_ds_pack_bwd(lb_ds_weights w, float* out) {
     out[i] = src ? src[in * 64 + row] : 0.f;
 }
 
+// ---- lb_ds_set_grads: out[m][n] = scale * sum_s A(s, m) B(s, n), one job per weight
+// gradient (fused_train.py's _over_sets and sums), the sets staged through LDS in chunks
+struct SetGradJob {
+    const float* a;  // amode 0: A(s, m) = a[s lda + m]; 1: A = 1; 2: A(s, 0) = sum_{r < alen} a[s lda + r]
+    int lda, M, amode, alen;
+    const float* b;  // B(s, n) = b[s ldb + n]
+    int ldb, N;
+    float scale;
+    float* out;      // [M][N]
+};
+constexpr int SG_JOBS = 8, SG_CH = 64, SG_THREADS = 256, SG_PER = SG_CH * 64 / SG_THREADS;
+struct SetGradParams {
+    SetGradJob job[SG_JOBS];
+    int64_t S;
+};
+
+// a chunk's loads are all issued before the first is used (the DQN's 128 sets: two chunks,
+// two memory round trips per block); the row sums take 4 lanes per set
+__global__ __launch_bounds__(SG_THREADS) void k_ds_set_grads(SetGradParams p) {
+    __shared__ float sa[SG_CH][64], sb[SG_CH][64];
+    const SetGradJob j = p.job[blockIdx.y];
+    const int tile = blockIdx.x * SG_THREADS;
+    if (tile >= j.M * j.N) return;  // (block-uniform)
+    const int e = tile + threadIdx.x;
+    const bool on = e < j.M * j.N;
+    const int m = on ? e / j.N : 0, n = on ? e % j.N : 0;
+    float acc = 0.f;
+    for (int64_t s0 = 0; s0 < p.S; s0 += SG_CH) {
+        const int cs = p.S - s0 < SG_CH ? (int)(p.S - s0) : SG_CH;
+        float rb[SG_PER], ra[SG_PER];
+#pragma unroll
+        for (int q = 0; q < SG_PER; ++q) {
+            const int i = threadIdx.x + q * SG_THREADS, s = i >> 6, c = i & 63;
+            rb[q] = (s < cs && c < j.N) ? j.b[(s0 + s) * j.ldb + c] : 0.f;
+            ra[q] = (s < cs && c < j.M && j.amode == 0) ? j.a[(s0 + s) * j.lda + c] : 1.f;
+        }
+        float rs = 0.f;
+        if (j.amode == 2) {  // lane (set threadIdx / 4, part threadIdx % 4): rows part, part + 4, ...
+            const int s = threadIdx.x >> 2, part = threadIdx.x & 3;
+            if (s < cs) {
+                const float* row = j.a + (s0 + s) * j.lda;
+                float t0 = 0.f, t1 = 0.f;
+                int r = part;
+                for (; r + 4 < j.alen; r += 8) {
+                    t0 += row[r];
+                    t1 += row[r + 4];
+                }
+                if (r < j.alen) t0 += row[r];
+                rs = t0 + t1;
+            }
+            rs += __shfl_xor(rs, 1);
+            rs += __shfl_xor(rs, 2);
+        }
+        __syncthreads();  // (the previous chunk is consumed)
+#pragma unroll
+        for (int q = 0; q < SG_PER; ++q) {
+            const int i = threadIdx.x + q * SG_THREADS;
+            sb[i >> 6][i & 63] = rb[q];
+            if (j.amode != 2 || (i & 63) != 0) sa[i >> 6][i & 63] = ra[q];  // (row sums: below)
+        }
+        if (j.amode == 2 && (threadIdx.x & 3) == 0 && (int)(threadIdx.x >> 2) < cs) sa[threadIdx.x >> 2][0] = rs;
+        __syncthreads();
+        if (on)
+            for (int s = 0; s < cs; ++s) acc += sa[s][m] * sb[s][n];
+    }
+    if (on) j.out[e] = j.scale * acc;
+}
+
 }  // namespace lbk

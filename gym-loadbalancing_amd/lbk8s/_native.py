@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblbk8s.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 LB_REWARD = {"naive": 0, "latency": 1, "fairness": 2, "multi": 3}
 LB_RNG_PHILOX, LB_RNG_TRACE = 0, 1
@@ -62,6 +62,7 @@ LB_DS_BWD_FLOATS = 24704
 LB_DS_SETVEC_FLOATS = 904
 LB_DS_WGRAD_FLOATS = 4608
 LB_DS_WORKSPACE_FLOATS = 1024 * 2 * LB_DS_WGRAD_FLOATS
+LB_DS_SETGRAD_ACTOR, LB_DS_SETGRAD_CRITIC = 4736, 12800
 LB_DSV = {"MAX0": 0, "GA3": 8, "MAX2A": 72, "GS2A": 136, "MAX1A": 200, "GS1A": 264, "CS2": 328,
           "MAX2C": 392, "GS2C": 456, "MAX1C": 520, "GS1C": 584, "ID1A": 648, "ID2A": 680, "ID1C": 712,
           "ID2C": 744, "P1A": 776, "P1C": 840}
@@ -119,11 +120,12 @@ def lib():
     L.lb_dqn_act.argtypes = [vp, vp, i64, i32, vp, vp, cfgp, C.POINTER(LBDQNExploreC), vp, vp]
     L.lb_dqn_head.argtypes = [vp, vp, vp, vp, vp, i64, i32, C.c_float, vp, vp, vp, vp, vp]
     L.lb_replay_sample.argtypes = [i64, i32, i64, i32, C.c_uint64] + [vp] * 12 + [vp]
+    L.lb_ds_set_grads.argtypes = [vp, vp, vp, i64, i32, vp, vp]
     for f in ("lb_validate_config", "lb_state_bytes", "lb_init", "lb_reset", "lb_step", "lb_policy", "lb_rollout",
               "lb_get_field", "lb_get_stats", "lb_status", "lb_ds_pack", "lb_ds_forward",
               "lb_ds_train_forward", "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax",
               "lb_replay_add", "lb_ppo_head", "lb_episode_log", "lb_dqn_act", "lb_dqn_head",
-              "lb_replay_sample"):
+              "lb_replay_sample", "lb_ds_set_grads"):
         getattr(L, f).restype = C.c_int
     v = L.lb_abi_version()
     if v != ABI_VERSION:
@@ -146,4 +148,4 @@ EXPORTED_SYMBOLS = ("lb_abi_version", "lb_last_error", "lb_validate_config", "lb
                     "lb_init", "lb_reset", "lb_step", "lb_policy", "lb_rollout", "lb_get_field", "lb_get_stats",
                     "lb_status", "lb_ds_pack", "lb_ds_forward", "lb_ds_train_forward",
                     "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax", "lb_replay_add", "lb_ppo_head",
-                    "lb_episode_log", "lb_dqn_act", "lb_dqn_head", "lb_replay_sample")
+                    "lb_episode_log", "lb_dqn_act", "lb_dqn_head", "lb_replay_sample", "lb_ds_set_grads")

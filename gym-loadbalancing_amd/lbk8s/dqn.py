@@ -211,6 +211,7 @@ class DQN_DeepSets:
         # the target network's image, packed when the target changes (every
         # target_network_frequency steps), outside the captured periods
         self._tfrag = fused.frag_buffer(self.device) if self.device_rng else None
+        self._one = None
 
     def select_actions(self, obs, masks, epsilon):
         if random.random() < epsilon:  # one draw decides exploration for every env (:127)
@@ -468,7 +469,10 @@ class DQN_DeepSets:
         # pool, at the same addresses every replay, and no zero fill + accumulate per parameter
         # is recorded)
         self.optimizer.zero_grad(set_to_none=True)
-        loss.backward()
+        # (the seed gradient from a fixed tensor: loss.backward() fills a new one each step)
+        if self._one is None or self._one.device != loss.device:
+            self._one = torch.ones((), dtype=loss.dtype, device=loss.device)
+        loss.backward(self._one)
         if self._multi and self.train_graph:
             torch.cat([p.grad.reshape(-1) for p in self.q_network.parameters()], out=self._gflat)
         return loss

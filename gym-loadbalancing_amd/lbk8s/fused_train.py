@@ -69,6 +69,10 @@ def _vec(setvec, name, n=64):
 
 
 SET_CHUNK = 512  # sets per partial product of a reduction over the sets
+# up to this many sets the small weight gradients are one lb_ds_set_grads launch (the DQN's
+# 128-set step: it replaces three GEMMs, two reductions and their fill / negation kernels);
+# above, the chunked GEMMs of _over_sets
+SET_GRADS_MAX_SETS = 512
 
 
 def _over_sets(a, b, alpha=1.0):
@@ -134,6 +138,18 @@ class _FusedDeepSetsTrain(torch.autograd.Function):
         _native.check(_native.lib().lb_ds_train_backward(
             bfrag.data_ptr(), x.data_ptr(), B, R, save_a.data_ptr(), fused._ptr(save_c), dlogits.data_ptr(),
             fused._ptr(dmean), wgrad.data_ptr(), work.data_ptr(), setvec.data_ptr(), _stream(dev)))
+        if B <= SET_GRADS_MAX_SETS:  # the sums over the sets in one launch (lb_ds_set_grads)
+            n = _native.LB_DS_SETGRAD_ACTOR + (_native.LB_DS_SETGRAD_CRITIC if critic is not None else 0)
+            sg = torch.empty(n, dtype=torch.float32, device=dev)
+            _native.check(_native.lib().lb_ds_set_grads(setvec.data_ptr(), dlogits.data_ptr(), fused._ptr(dmean),
+                                                        B, R, sg.data_ptr(), _stream(dev)))
+            grads = [wgrad[0, 4096:].view(64, 8), sg[:512].view(64, 8), wgrad[0, :4096].view(64, 64),
+                     sg[512:4608].view(64, 64), sg[4608:4672].view(1, 64), sg[4672:4736].view(1, 64)]
+            if critic is not None:
+                c = sg[_native.LB_DS_SETGRAD_ACTOR:]
+                grads += [wgrad[1, 4096:].view(64, 8), c[:512].view(64, 8), wgrad[1, :4096].view(64, 64),
+                          c[512:4608].view(64, 64), c[4608:8704].view(64, 64), c[8704:].view(64, 64)]
+            return (None, None, None, None) + tuple(grads)
         max0 = _vec(setvec, "MAX0", 8)
         g3 = dlogits.sum(1)
         grads = [
@@ -230,11 +246,14 @@ class _PPOHead(torch.autograd.Function):
         ctx.vshape = value.shape
         stats = means[:5]
         ctx.mark_non_differentiable(stats)
+        ctx.set_materialize_grads(False)  # (no zero fill for the stats' gradient)
         return means[5], stats
 
     @staticmethod
     def backward(ctx, gloss, gstats):
         dlogits, dvalue = ctx.saved_tensors
+        if gloss is None:
+            return (None,) * 12
         return (dlogits * gloss, (dvalue * gloss).view(ctx.vshape)) + (None,) * 10
 
 
@@ -265,11 +284,16 @@ class _DQNHead(torch.autograd.Function):
             td.data_ptr(), old.data_ptr(), _stream(dev)))
         ctx.save_for_backward(dq)
         ctx.mark_non_differentiable(td, old)
+        # (td and old get no gradient: without this autograd fills two zero tensors for them,
+        # two kernels per DQN train step)
+        ctx.set_materialize_grads(False)
         return sq.mean(), td, old
 
     @staticmethod
     def backward(ctx, gloss, gtd, gold):
         (dq,) = ctx.saved_tensors
+        if gloss is None:
+            return (None,) * 6
         return dq * gloss, None, None, None, None, None
 
 

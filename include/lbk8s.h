@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LBK8S_ABI_VERSION 6
+#define LBK8S_ABI_VERSION 7
 
 /* reward_function names of loadbalancer_k8s_env.py:20-31 */
 enum { LB_REWARD_NAIVE = 0, LB_REWARD_LATENCY = 1, LB_REWARD_FAIRNESS = 2, LB_REWARD_MULTI = 3 };
@@ -378,6 +378,20 @@ int lb_ds_train_backward(const float* bwd_frag, const float* obs, int64_t num_en
                          const float* save_actor, const float* save_critic, const float* dlogits,
                          const float* dmean, float* wgrad_out, float* workspace, float* setvec,
                          void* stream);
+
+/* The remaining weight gradients listed above (the sums over the sets) in one launch, for
+ * small batches: the DQN's 128-set train step ran them as three GEMMs, two reductions and
+ * their fill / negation kernels.  out = actor dGamma1 [64][8], dGamma2 [64][64], dLambda3
+ * [64], dGamma3 [64] (LB_DS_SETGRAD_ACTOR floats), then, when dmean is non-NULL, critic
+ * dGamma1 [64][8], dGamma2 [64][64], dLambda3 [64][64], dGamma3 [64][64]
+ * (LB_DS_SETGRAD_CRITIC more).  setvec: after lb_ds_train_backward; dlogits [B,R]; dmean
+ * [B,64] or NULL.  Each output is one thread's sum over the sets in ascending order
+ * (deterministic); the work per output grows with num_sets (the GEMM formulation is the
+ * one for large batches). */
+#define LB_DS_SETGRAD_ACTOR 4736
+#define LB_DS_SETGRAD_CRITIC 12800
+int lb_ds_set_grads(const float* setvec, const float* dlogits, const float* dmean, int64_t num_sets,
+                    int32_t num_elements, float* out, void* stream);
 
 #ifdef __cplusplus
 }

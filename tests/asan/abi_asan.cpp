@@ -100,8 +100,12 @@ int main() {
                       nullptr) != 0);
     CHECK(lb_replay_sample(1, 72, 4, 8, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                            nullptr, nullptr, nullptr, nullptr, nullptr) != 0);
+    CHECK(lb_ds_set_grads(nullptr, nullptr, nullptr, 1, 9, nullptr, nullptr) != 0);
     // out-of-range arguments past the NULL checks (fake, never-dereferenced pointers)
     void* fake = reinterpret_cast<void*>(0x1000);
+    CHECK(lb_ds_set_grads((const float*)fake, (const float*)fake, nullptr, 1, LB_DS_MAX_ELEMENTS_TRAIN + 1,
+                          (float*)fake, nullptr) != 0);
+    CHECK(lb_ds_set_grads((const float*)fake, (const float*)fake, nullptr, 0, 9, (float*)fake, nullptr) != 0);
     CHECK(lb_policy(fake, &c, 16, 9, (int32_t*)fake, nullptr) != 0);
     CHECK(lb_get_field(fake, &c, 16, LB_FIELD_COUNT, (double*)fake, nullptr) != 0);
     CHECK(lb_get_field(fake, &c, 16, LB_FIELD_DT, (double*)fake, nullptr) != 0);

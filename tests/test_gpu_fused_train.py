@@ -104,6 +104,31 @@ def test_train_step_actor_only_and_many_sets():
         _check(p.grad, r.grad, f"grad {name}", 1e-3, 1e-4)
 
 
+@pytest.mark.parametrize("B,R,critic", [(1, 9, True), (128, 9, False), (128, 65, True), (300, 257, False),
+                                         (512, 17, True)])
+def test_set_grads_kernel_matches_gemm_path(B, R, critic, monkeypatch):
+    """lb_ds_set_grads (the small-batch path: one launch) against the chunked GEMMs and
+    reductions of _over_sets on the same backward (both f32; rtol 1e-5)."""
+    from lbk8s import fused_train
+    from lbk8s.deepsets import DQNDeepSetAgent
+    x = _inputs(B, R, seed=B + R).cuda()
+    w = torch.randn(B, R, generator=torch.Generator().manual_seed(B)).cuda()
+    grads = []
+    for limit in (fused_train.SET_GRADS_MAX_SETS, 0):
+        monkeypatch.setattr(fused_train, "SET_GRADS_MAX_SETS", limit)
+        if critic:
+            agent = _agent(R).cuda()
+            logits, value = fused_train.actor_critic(agent, x)
+            ((logits * w).sum() + (value * w[:, 0]).sum()).backward()
+        else:
+            torch.manual_seed(R)
+            agent = DQNDeepSetAgent(8).cuda()
+            (fused_train.actor_only(agent, agent.q_network.net, x) * w).sum().backward()
+        grads.append([p.grad.clone() for p in agent.parameters()])
+    for i, (a, b) in enumerate(zip(*grads)):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6 * float(b.abs().max()) + 1e-12, msg=f"param {i}")
+
+
 def test_train_forward_caches_follow_updates():
     """Two optimizer steps: the forward image is repacked (parameter versions move)."""
     from lbk8s import fused_train
