@@ -5,6 +5,10 @@ staggered env batches: obs, reward, done, actions, terminal obs, episode stats a
 env state words after three launches must be bit-identical.
 
     python tools/persist_check.py [--envs 300001] [--K 20] [--variant 11]
+
+(Variant 11 was measured slower and removed from liblbk8s.so, profiles/r03_ablation.jsonl;
+an unknown variant number runs the product dispatch, so the check now compares it with
+itself: keep the script for the next launch-scheduling experiment.)
 """
 import argparse
 import ctypes as C
