@@ -333,9 +333,13 @@ class DQN_DeepSets:
 
     def _train_warmup(self):
         """Two train steps on a side stream (grads, Adam state, workspaces allocated before a
-        capture), then the parameters and Adam state restored: nothing is drawn."""
+        capture), then the parameters and the Adam state (moments and step counter) restored
+        to their values before the warm-up: nothing is drawn.  (The period graphs are rebuilt
+        whenever a learn() changes the exploration slope; training continues from the same
+        optimizer state.)"""
         params = list(self.q_network.parameters())
         snap = [p.detach().clone() for p in params]
+        opt_snap = self._snapshot_optimizer()
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
@@ -347,10 +351,7 @@ class DQN_DeepSets:
         with torch.no_grad():
             for p, q in zip(params, snap):
                 p.copy_(q)
-            for st in self.optimizer.state.values():
-                for v in st.values():
-                    if isinstance(v, torch.Tensor):
-                        v.zero_()
+        self._restore_optimizer(opt_snap)
         fused.invalidate(self.q_network)
 
     def _after_train(self, global_step):
@@ -394,6 +395,12 @@ class DQN_DeepSets:
             # (captured, not run: the env, replay and counters are untouched)
             self._pgraphs = self._build_period_graphs(obs, masks)
             self._pgraph_slope = slope
+        # the replay's device slot lives in pos_pp[parity]: after a learn() with an odd number
+        # of vector steps it is in word 1, so move it to word 0 with the parity (a second
+        # learn() would otherwise rewrite the last transition and run one slot behind the
+        # host's pos)
+        if self._parity:
+            self.rb.pos_pp[0].copy_(self.rb.pos_pp[1])
         self._parity = 0
         self._vstep_pp.zero_()
         self._base_adds.fill_(self.rb.size if self.rb.full else self.rb.pos)
@@ -490,7 +497,7 @@ class DQN_DeepSets:
     def _capture_train(self):
         """Capture the train step on fixed sample buffers: one graph on one rank, two graphs
         around the gradient all_reduce on several (as PPO's minibatch step).  The warm-up
-        steps are undone (parameters restored, Adam state zeroed) and draw nothing from the
+        steps are undone (parameters and Adam state restored) and draw nothing from the
         sampling generator, so a graphed run trains exactly as an eager one."""
         B, rb = self.batch_size, self.rb
         obs_shape = tuple(rb.obs.shape[2:])
@@ -500,6 +507,7 @@ class DQN_DeepSets:
                          torch.zeros((B, 1), device=self.device), torch.zeros((B, 1), device=self.device))
         params = list(self.q_network.parameters())
         snap = [p.detach().clone() for p in params]
+        opt_snap = self._snapshot_optimizer()
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
@@ -524,11 +532,26 @@ class DQN_DeepSets:
         with torch.no_grad():
             for p, q in zip(params, snap):
                 p.copy_(q)
-            for st in self.optimizer.state.values():
-                for v in st.values():
-                    if isinstance(v, torch.Tensor):
-                        v.zero_()
+        self._restore_optimizer(opt_snap)
         fused.invalidate(self.q_network)
+
+    def _snapshot_optimizer(self):
+        """Copies of the Adam state tensors (moments, step) by parameter, before a warm-up."""
+        return {id(p): {k: v.detach().clone() for k, v in st.items() if isinstance(v, torch.Tensor)}
+                for p, st in self.optimizer.state.items()}
+
+    def _restore_optimizer(self, saved):
+        """Undo a warm-up's optimizer steps: state that existed before it gets its values
+        back, state the warm-up created (a fresh optimizer) is zeroed (step 0, zero moments)."""
+        with torch.no_grad():
+            for p, st in self.optimizer.state.items():
+                old = saved.get(id(p), {})
+                for k, v in st.items():
+                    if isinstance(v, torch.Tensor):
+                        if k in old:
+                            v.copy_(old[k])
+                        else:
+                            v.zero_()
 
     def _allreduce(self):
         if self._multi and self.train_graph:

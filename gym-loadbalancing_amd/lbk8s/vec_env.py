@@ -117,8 +117,10 @@ class _MonitorWriter:
         for row, tt in zip(rows, t):
             info = step_info(row[:_native.LB_ST_K], float(row[_native.LB_EPLOG_REWARD]),
                              int(row[_native.LB_EPLOG_ACTION]))
+            # VecMonitor writes its float32 running return as it stands (str of the float32,
+            # no rounding; only the time is rounded to 6 places)
             r32 = np.float32(row[_native.LB_EPLOG_RET32])
-            self.w.writerow([round(r32, 6), int(row[ST_LENGTH]), round(tt - self.t_start, 6)]
+            self.w.writerow([r32, int(row[ST_LENGTH]), round(tt - self.t_start, 6)]
                             + [info[k] for k in self.keys])
         self.f.flush()
 

@@ -189,6 +189,73 @@ def test_gae_matches_direct_recursion():
     assert torch.allclose(ret, adv + v)
 
 
+def _gae_fixture():
+    import os
+    return np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "nn_gae.npz"))
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_gae_matches_reference_learn(device):
+    """compute_gae (lbk8s/ppo.py) against the advantages / returns the reference's own
+    PPO_DeepSets.learn() computed (ppo_deepset.py:192-205) on the storage its rollout loop
+    filled (tests/golden/gen_golden_gae.py: reference envs, multi reward, dones at staggered
+    steps).  Same float32 tensor ops in the same order: bit for bit on the CPU, 1e-6 on the
+    GPU."""
+    from lbk8s.ppo import compute_gae
+    d = _gae_fixture()
+    t = {k: torch.from_numpy(d[k]).to(device) for k in ("rewards", "values", "dones", "next_value", "next_done")}
+    adv, ret = compute_gae(t["rewards"], t["values"], t["dones"], t["next_value"], t["next_done"],
+                           float(d["gamma"]), float(d["gae_lambda"]))
+    adv, ret = adv.cpu().numpy(), ret.cpu().numpy()
+    if device == "cpu":
+        assert np.array_equal(adv, d["advantages"]) and np.array_equal(ret, d["returns"])
+    else:
+        np.testing.assert_allclose(adv, d["advantages"], rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(ret, d["returns"], rtol=1e-6, atol=1e-6)
+
+
+def test_ppo_storage_sequencing_matches_reference_learn():
+    """learn()'s storage convention (ppo_deepset.py:162-176): dones[t] is the done flag that
+    came back from step t - 1 (zeros at t = 0), rewards[t] the reward of step t, next_done the
+    flags of the last step.  The reference fixture shows it; PPO_DeepSets._rollout_body (our
+    rollout) fills its storage the same way when its env returns the reference's per-step
+    rewards and dones."""
+    from lbk8s.ppo import PPO_DeepSets
+    d = _gae_fixture()
+    raw = d["raw_dones"].astype(np.float32)
+    T, B = raw.shape
+    assert np.array_equal(d["dones"][0], np.zeros(B, np.float32))
+    assert np.array_equal(d["dones"][1:], raw[:-1]) and np.array_equal(d["next_done"], raw[-1])
+
+    class _Space:
+        def __init__(self, shape, n=None):
+            self.shape, self.n = shape, n
+
+    class StubEnv:  # returns the reference's step outputs in order
+        num_envs, device = B, torch.device("cpu")
+        observation_space, action_space = _Space((7, 8)), _Space((), 7)
+        ep_stats = torch.zeros((B, 16), dtype=torch.float64)
+
+        def __init__(self):
+            self.t = 0
+
+        def step_device(self, act, obs_out, reward_out, done_out):
+            obs_out.zero_()
+            reward_out.copy_(torch.from_numpy(d["rewards"][self.t]))
+            done_out.copy_(torch.from_numpy(d["raw_dones"][self.t].astype(np.uint8)))
+            self.t += 1
+
+        def record_episodes(self, *a):
+            pass
+
+    algo = PPO_DeepSets(StubEnv(), num_steps=T, n_minibatches=2, update_epochs=1, seed=2, device="cpu",
+                        use_graphs=False)
+    next_done = algo._rollout_body(torch.zeros(B))
+    assert np.array_equal(algo.dones.numpy(), d["dones"])
+    assert np.array_equal(algo.rewards.numpy(), d["rewards"])
+    assert np.array_equal(next_done.numpy(), d["next_done"])
+
+
 def test_equivariant_custom_backward_gradcheck():
     """The GPU training path's hand-written backward (_EquivariantFn) against numerical
     gradients, float64 on the CPU; inputs include exact ties in the set-wise max (as the

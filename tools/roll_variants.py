@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--lib", default=None, help="another build of liblbk8s.so (an A/B across builds)")
     ap.add_argument("--no-obs", action="store_true", help="launch without the obs output (compute + small outputs)")
     ap.add_argument("--slot0", action="store_true", help="every timed launch writes from ring slot 0")
+    ap.add_argument("--lockstep", action="store_true",
+                    help="no staggering: every env restarts before each measurement (no episode ends "
+                         "inside warm-up + timed launches when (launches + 1) * K < L)")
     args = ap.parse_args()
     import torch
 
@@ -55,7 +58,7 @@ def main():
         done.zero_()
     env.reset()
     gid = torch.arange(B, device=dev)
-    for r in range(1, EL):
+    for r in range(1, 1 if args.lockstep else EL):
         env.step_device(None, obs_out=obs[0], reward_out=rew[0], done_out=done[0])
         env.reset_masked((gid % EL) == r)
     stream = torch.cuda.current_stream(dev)
@@ -63,6 +66,8 @@ def main():
         for K in [int(x) for x in args.steps.split(",")]:
             for var, stg in [(v, g) for v in [int(x) for x in args.variants.split(",")] for g in staggers]:
                 L.lbx_set_rollout_variant(var)
+                if args.lockstep:
+                    env.reset()
                 env.rollout("random", K, obs_out=obs[0], reward_out=rew[0], done_out=done[0])  # warm
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -75,7 +80,7 @@ def main():
                 torch.cuda.synchronize()
                 us_launch = e0.elapsed_time(e1) * 1e3 / args.launches
                 us = us_launch / max(K, 1)
-                print(json.dumps({"rep": rep, "K": K, "variant": var, "stagger": stg,
+                print(json.dumps({"rep": rep, "K": K, "variant": var, "stagger": stg, "lockstep": args.lockstep,
                                   "lib": os.path.basename(_native.LIB_PATH),
                                   "envs": B, "us_per_launch": round(us_launch, 2), "us_per_step": round(us, 2),
                                   "env_steps_per_s": B * K / us_launch * 1e6}), flush=True)
