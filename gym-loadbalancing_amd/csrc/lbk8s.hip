@@ -28,6 +28,7 @@
 #include "lbk8s_slice.h"
 #include "lbk8s_tpe.h"
 #include "lbk8s_rollout.h"
+#include "lbk8s_lean.h"
 
 namespace lbk {
 
@@ -305,9 +306,14 @@ __global__ void k_status(Params p, uint32_t* flags) {
 
 // ---- host side ---------------------------------------------------------------------------
 thread_local std::string g_err;
-// experiment switch (lbx_set_rollout_variant, tools/roll_variants.py): 3 = the round-2
-// k_rollout_tpe for the L >= K launches k_rollout_img serves (an A/B reference)
+#ifdef LB_EXPERIMENTS
+// experiment switch of a diagnostic build (-DLB_EXPERIMENTS; lbx_set_rollout_variant,
+// tools/roll_variants.py): 1 = k_rollout_img where k_rollout_lean would run, 3 = k_rollout_tpe
+// for every L >= K launch (A/B references)
 int g_rollout_variant = 0;
+#else
+constexpr int g_rollout_variant = 0;
+#endif
 
 int fail(const char* msg) {
     g_err = msg;
@@ -520,6 +526,29 @@ int device_cus() {
     return cus;
 }
 
+// Which kernel lb_rollout launches (lb_rollout_kernel reports it, LB_ROLLOUT_*).
+// Per-lane addresses of the thread-per-env rollouts are 32-bit byte offsets from scalar bases
+// (k_rollout_img: the state blob and the ep_stats rows; k_rollout_lean also the obs slot and
+// the terminal observations), so they run only while every such offset fits in 32 bits; larger
+// launches take k_rollout_tpe, which indexes in 64 bits.
+int rollout_kernel(const lb_config* c, int64_t B, int32_t steps, bool outputs_all) {
+    const Geo g = geometry(c, B);
+    if (!g.tpe) return LB_ROLLOUT_SLICE;
+    if (g.NZW > 2) return LB_ROLLOUT_STEPS;
+    const bool pre = c->auto_reset && c->episode_length >= steps;
+    if (!pre) return LB_ROLLOUT_TPE;
+    const uint64_t lim = 0xFFFFFFFFull;
+    const int R = c->num_endpoints + (c->rejection_allowed ? 1 : 0);
+    const bool img_fits = offsets(c, B).end <= lim && (uint64_t)B * LB_ST_K * 8 <= lim;
+    const bool lean_fits = img_fits && (uint64_t)B * R * 32 <= lim;
+    const bool lean_shape = (c->num_endpoints == 8 && R == 9 && c->num_nodes <= 32) ||
+                            (c->num_endpoints == 6 && R == 7 && c->num_nodes <= 64);
+    if (lean_fits && lean_shape && B % 64 == 0 && B > SMALL_TPE_MAX_B && outputs_all && g_rollout_variant == 0)
+        return LB_ROLLOUT_LEAN;
+    if (img_fits && g_rollout_variant != 3) return LB_ROLLOUT_IMG;
+    return LB_ROLLOUT_TPE;
+}
+
 }  // namespace lbk
 
 using namespace lbk;
@@ -528,7 +557,14 @@ extern "C" {
 
 int lb_abi_version(void) { return LBK8S_ABI_VERSION; }
 
+#ifndef LBK8S_SRC_HASH
+#define LBK8S_SRC_HASH "unhashed"  // built outside the Makefile
+#endif
+const char* lb_source_hash(void) { return LBK8S_SRC_HASH; }
+
+#ifdef LB_EXPERIMENTS
 int lbx_set_rollout_variant(int v) { g_rollout_variant = v; return 0; }
+#endif
 #ifdef LB_TIMELINE
 int lbx_set_timeline(uint64_t* buf) { return hipMemcpyToSymbol(HIP_SYMBOL(g_timeline), &buf, sizeof(buf)) == hipSuccess ? 0 : -1; }
 #endif
@@ -639,6 +675,14 @@ int lb_step(void* state, const lb_config* cfg, int64_t num_envs, const int32_t* 
     return check_launch();
 }
 
+int lb_rollout_kernel(const lb_config* cfg, int64_t num_envs, int32_t steps, int32_t outputs_all,
+                      int32_t* kernel_out) {
+    if (int r = validate(cfg)) return r;
+    if (num_envs < 1 || steps < 0 || !kernel_out) return fail("num_envs < 1, steps < 0 or kernel_out NULL");
+    *kernel_out = rollout_kernel(cfg, num_envs, steps, outputs_all != 0);
+    return 0;
+}
+
 int lb_rollout(void* state, const lb_config* cfg, int64_t num_envs, int32_t policy, int32_t steps,
                float* obs_out, float* reward_out, uint8_t* done_out, int32_t* actions_out,
                float* terminal_obs_out, double* ep_stats_out, void* stream) {
@@ -661,7 +705,27 @@ int lb_rollout(void* state, const lb_config* cfg, int64_t num_envs, int32_t poli
         // episodes at least as long as the launch (an env ends at most once in it): next
         // episodes drawn before the first step
         const bool pre = cfg->auto_reset && cfg->episode_length >= steps;
-        if (pre && g_rollout_variant != 3) {  // k_rollout_img (lbk8s_rollout.h)
+        const int rk = rollout_kernel(cfg, num_envs, steps, obs_out && reward_out && done_out && terminal_obs_out &&
+                                                                ep_stats_out);
+        if (rk == LB_ROLLOUT_LEAN) {  // k_rollout_lean (lbk8s_lean.h)
+            const bool e8 = p.E == 8, naive = p.reward_fn == LB_REWARD_NAIVE, act = actions_out != nullptr;
+#define LB_LEAN(KIND_, ET_, RT_, NZW_)                                                                           \
+            if (naive && act) hipLaunchKernelGGL((k_rollout_lean<KIND_, ET_, RT_, NZW_, true, true>), grid, block, 0, s, p, (int)steps, actions_out); \
+            else if (naive) hipLaunchKernelGGL((k_rollout_lean<KIND_, ET_, RT_, NZW_, true, false>), grid, block, 0, s, p, (int)steps, actions_out); \
+            else if (act) hipLaunchKernelGGL((k_rollout_lean<KIND_, ET_, RT_, NZW_, false, true>), grid, block, 0, s, p, (int)steps, actions_out); \
+            else hipLaunchKernelGGL((k_rollout_lean<KIND_, ET_, RT_, NZW_, false, false>), grid, block, 0, s, p, (int)steps, actions_out);
+#define LB_LEAN_KIND(KIND_) if (e8) { LB_LEAN(KIND_, 8, 9, 1) } else { LB_LEAN(KIND_, 6, 7, 2) }
+            switch (policy) {
+            case LB_POLICY_TOPOLOGY_GREEDY: LB_LEAN_KIND(LB_POLICY_TOPOLOGY_GREEDY); break;
+            case LB_POLICY_ZONE_CPU_GREEDY: LB_LEAN_KIND(LB_POLICY_ZONE_CPU_GREEDY); break;
+            case LB_POLICY_ENDPOINT_CPU_GREEDY: LB_LEAN_KIND(LB_POLICY_ENDPOINT_CPU_GREEDY); break;
+            default: LB_LEAN_KIND(LB_POLICY_RANDOM); break;
+            }
+#undef LB_LEAN_KIND
+#undef LB_LEAN
+            return check_launch();
+        }
+        if (rk == LB_ROLLOUT_IMG) {  // k_rollout_img (lbk8s_rollout.h)
             const bool e8 = p.E == 8 && p.R == 9;
 #define LB_IMG(NB_, KIND_)                                                                                   \
             if (e8) hipLaunchKernelGGL((k_rollout_img<NB_, KIND_, 8, 9, 4>), grid, block, 0, s, p, (int)steps, actions_out); \
@@ -677,20 +741,20 @@ int lb_rollout(void* state, const lb_config* cfg, int64_t num_envs, int32_t poli
 #undef LB_IMG
             return check_launch();
         }
-#define LB_ROLLOUT_TPE_NB(NB_, KIND_)                                                                         \
+#define LB_TPE_NB(NB_, KIND_)                                                                         \
         if (pre) hipLaunchKernelGGL((k_rollout_tpe<NB_, KIND_, true>), grid, block, 0, s, p, (int)steps, actions_out); \
         else hipLaunchKernelGGL((k_rollout_tpe<NB_, KIND_, false>), grid, block, 0, s, p, (int)steps, actions_out);
-#define LB_ROLLOUT_TPE(KIND_)                         \
-        if (small) { LB_ROLLOUT_TPE_NB(64, KIND_) }   \
-        else { LB_ROLLOUT_TPE_NB(BLOCK, KIND_) }
+#define LB_TPE_KIND(KIND_)                         \
+        if (small) { LB_TPE_NB(64, KIND_) }   \
+        else { LB_TPE_NB(BLOCK, KIND_) }
         switch (policy) {
-        case LB_POLICY_TOPOLOGY_GREEDY: LB_ROLLOUT_TPE(LB_POLICY_TOPOLOGY_GREEDY); break;
-        case LB_POLICY_ZONE_CPU_GREEDY: LB_ROLLOUT_TPE(LB_POLICY_ZONE_CPU_GREEDY); break;
-        case LB_POLICY_ENDPOINT_CPU_GREEDY: LB_ROLLOUT_TPE(LB_POLICY_ENDPOINT_CPU_GREEDY); break;
-        default: LB_ROLLOUT_TPE(LB_POLICY_RANDOM); break;
+        case LB_POLICY_TOPOLOGY_GREEDY: LB_TPE_KIND(LB_POLICY_TOPOLOGY_GREEDY); break;
+        case LB_POLICY_ZONE_CPU_GREEDY: LB_TPE_KIND(LB_POLICY_ZONE_CPU_GREEDY); break;
+        case LB_POLICY_ENDPOINT_CPU_GREEDY: LB_TPE_KIND(LB_POLICY_ENDPOINT_CPU_GREEDY); break;
+        default: LB_TPE_KIND(LB_POLICY_RANDOM); break;
         }
-#undef LB_ROLLOUT_TPE
-#undef LB_ROLLOUT_TPE_NB
+#undef LB_TPE_KIND
+#undef LB_TPE_NB
         return check_launch();
     }
     if (g.tpe) {  // thread-per-env layout, N > 64: K policy + step launches

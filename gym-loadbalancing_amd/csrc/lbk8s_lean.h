@@ -1,0 +1,676 @@
+// lbk8s_lean.h — k_rollout_lean: lb_rollout on the thread-per-env layout for the bench's and
+// config 1's launches (E = 8 / R = 9 with N <= 32 and E = 6 / R = 7 with N <= 64, episodes at
+// least as long as the launch, whole waves of 64 envs, every output written).
+//
+// k_rollout_img's step (lbk8s_rollout.h: one lane per env for the whole launch, the 40-word
+// LDS image of the observation rows, the next episodes drawn before the first step),
+// re-laid around one rule of the memory pipeline (MI355X_MICROARCH.md):
+//
+//   s_waitcnt vmcnt(N) retires a wave's vector-memory operations in ISSUE order, stores
+//   included, so the data of a load waits for every store its wave issued before it.
+//
+// A step stores ~19 KB per wave (obs block, rewards, done flags).  Every load of the loop is
+// therefore issued BEFORE the stores it would otherwise wait behind:
+//   * step k + 1's 4 table gathers right after its action, step k's obs / reward / done /
+//     action stores after them (spread over step k + 1's request draws);
+//   * the record of an env that ends at step k + 1 (the next episode, drawn before the first
+//     step) is fetched in iteration k, next to the gathers: 10 lanes x 16 bytes per env, one
+//     load instruction for up to 6 envs, landing in 4 registers per lane; at its end the wave
+//     drops it into the env's own image region and the env restarts from there, in place;
+//   * the terminal observations leave as one store per group of 64 / 2R envs (lane = piece),
+//     the episode-statistics row as 8 paired 16-byte stores.
+// Addresses are scalar buffer descriptors plus 32-bit lane offsets (raw buffer
+// instructions): no 64-bit per-lane address lives in a register, and the compiler cannot
+// strength-reduce the per-step output addresses into per-lane pointers.
+// Compile-time E, R, node-zone words and reward kind keep registers and SGPRs down.
+// The record layout is this kernel's own (lean_write_record: scenario words first, the
+// initial latencies last, so the in-place restart never overwrites a word it still needs).
+// Bit for bit K x (lb_policy + lb_step) and the C oracle (tests/test_gpu_api.py,
+// tests/test_gpu_parity.py): the same draws and float64 operations in the same order.
+#pragma once
+
+#include "lbk8s_rollout.h"
+
+namespace lbk {
+
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// raw buffer descriptor over [base, base + 4 GiB): stride 0, gfx9 data format word
+__device__ __forceinline__ Rsrc rsrc_of(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, -1, 0x00020000);
+}
+constexpr int BUF_NT = 2;  // cache-policy bit of a nontemporal access (gfx940+: sc0 = 1, nt = 2)
+
+__device__ __forceinline__ double buf_ld_f64(Rsrc r, uint32_t off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+__device__ __forceinline__ uint4 buf_ld_u128(Rsrc r, uint32_t off) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+#ifndef LB_ST_NOP
+#define LB_ST_NOP "s_nop 1"
+#endif
+template <int AUX>
+__device__ __forceinline__ void buf_st_f4(float4 v, Rsrc r, uint32_t voff, uint32_t soff) {
+    const u32x4 d{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+    __builtin_amdgcn_raw_buffer_store_b128(d, r, voff, soff, AUX);
+    // the store's data registers stay untouched for 2 wait states after it: with an SGPR
+    // soffset the compiler's hazard recognizer allows the next instruction to overwrite them
+    // (its rule for >64-bit buffer stores excludes that form), and on gfx950 that corrupted
+    // the stored data of a quarter of the lanes under load
+    asm volatile(LB_ST_NOP ::"v"(d.x), "v"(d.y), "v"(d.z), "v"(d.w));
+}
+
+// draw() with the Philox key laundered through an opaque copy: the 10 rounds' keys are then
+// recomputed by 2 scalar adds per round in every call instead of being hoisted out of the step
+// loop as 20 SGPRs (which spilled, and were read back with v_readlane in every round)
+__device__ __forceinline__ U4 draw_o(const Params& p, int64_t env, uint32_t episode, uint32_t slot, uint32_t dom) {
+    uint32_t k0 = p.key0, k1 = p.key1;
+    asm volatile("" : "+s"(k0), "+s"(k1));
+    const uint64_t gid = (uint64_t)(p.env_id_offset + env);
+    return philox((uint32_t)gid, episode, slot, dom | ((uint32_t)(gid >> 32) << 8), k0, k1);
+}
+template <int KIND>
+__device__ __forceinline__ int lean_policy(const Params& p, int64_t env, const TEnv& tv, const uint32_t (&em)[TPE_E],
+                                           const uint32_t (&ed)[TPE_E]) {
+    if constexpr (KIND == LB_POLICY_RANDOM) {  // random_action's draw
+        const U4 w = draw_o(p, env, (uint32_t)(tv.acc3 >> 32), (uint32_t)tv.s.step, D_ACT);
+        return (int)bounded(w.x, (uint32_t)p.A);
+    }
+    return tpe_policy<KIND>(p, env, tv, em, ed);
+}
+
+// topology latency between zones a and b (topo_val), branch-free
+__device__ __forceinline__ int topo_bf(uint64_t topo, int a, int b) {
+    const int i = a < b ? a : b, j = a < b ? b : a;
+    const int val = (int)((topo >> (9 * ((i * (7 - i)) / 2 + j - i - 1))) & 0x1FF);
+    return a == b ? 1 : val;
+}
+
+// the next step, prepared: its action with the request's threshold index and zone packed
+// in one word (a | thr_idx << 8 | rz << 12; the on-device policies draw a in [0, A)), the
+// selected endpoint's 4 table values, and next_request()'s clock already advanced (arrival
+// and dt from the clock the step will see: nothing changes it in between)
+struct LPrepL {
+    uint32_t arz;
+    double sel_lat, sel_cpu, next_lat, next_cpu, arr;
+    float dt;
+};
+
+// lean_apply with the packed preparation (the same operations in the same order)
+template <int ET, int RT, int RF>
+__device__ __forceinline__ double lean_apply_l(const Params& p, const LPrepL& pr, LEnv& v,
+                                               const uint32_t (&em)[TPE_E], uint32_t (&ed)[TPE_E], uint32_t* me) {
+    constexpr int E = ET;
+    const int rf = RF >= 0 ? RF : p.reward_fn;
+    const int a = (int)(pr.arz & 0xFFu);
+    const bool accept = a < E, reject = a == E;
+    const int ai = accept ? a : 0;
+    if (!((v.s1 >> S1_RD) & 1)) v.s1 |= 1u << S1_BAD;
+    const uint32_t emA = pick8(em, ai), edA = pick8(ed, ai);
+    const int oA = em_owner(emA);
+    const uint32_t edO = pick8(ed, oA);
+    const int jA = ed_j(edA);
+    const int Mn = ed_M(edO) < CMAX ? ed_M(edO) + 1 : CMAX;
+    const int jn = jA < CMAX ? jA + 1 : CMAX;
+    double reward;
+    if (accept) {
+        int cnt = 0;  // #{e != ai : loads[e] <= loads[ai]} for the O(E) Gini update
+#pragma unroll
+        for (int e = 0; e < TPE_E; ++e)
+            if (e < E && e != ai && ed_j(ed[e]) <= jA) ++cnt;
+        const int rz = (int)((v.s1 >> S1_RZ) & 3), zA = em_zone(emA);
+        const int tl = topo_bf(v.topo, rz, zA);
+        const uint32_t gnum = (uint32_t)(v.acc2 >> 32) + (uint32_t)(2 * (2 * cnt - (E - 1)));
+        v.acc2 = ((uint64_t)gnum << 32) | (uint32_t)((uint32_t)v.acc2 + (uint32_t)tl);
+        v.acc3 += (uint64_t)node_cost(em_type(emA));
+        v.s0 += 1u << 16;                 // acc (<= step <= L <= 1023: no saturation)
+        if (rz == zA) v.s1 += 1;          // intra
+        xsum_add(v.sum_lat, v.sum_cpu, v.sum_hi, pr.sel_lat, pr.sel_cpu, tl, rz != zA);
+        const uint32_t edA_new = ((oA == ai ? (uint32_t)Mn : (uint32_t)ed_M(edA)) << 20) |
+                                 ((uint32_t)Mn << 10) | (uint32_t)jn;
+#pragma unroll
+        for (int e = 0; e < TPE_E; ++e) {  // select-stores over constant indices
+            const uint32_t edo = e == oA ? (ed[e] & ~(0x3FFu << 20)) | ((uint32_t)Mn << 20) : ed[e];
+            ed[e] = e == ai ? edA_new : edo;
+        }
+        img_sel(me, ai, (float)pr.next_cpu, (float)pr.next_lat);
+        v.s1 &= ~(1u << S1_PEN);
+        reward = rf == LB_REWARD_NAIVE ? 1.0 : accept_reward(p, pr.sel_lat, tl, pr.sel_cpu, v.acc2, (int)(v.s0 >> 16));
+        v.last_r = reward;
+    } else if (reject) {
+        v.s1 |= 1u << S1_PEN;
+        reward = rf == LB_REWARD_LATENCY ? -1000.0 : -1.0;
+        v.last_r = reward;
+    } else {  // unrecognised action (:685-686): penalty and selected_* stay stale
+        reward = rf == LB_REWARD_NAIVE ? (((v.s1 >> S1_PEN) & 1) ? -1.0 : 1.0) : v.last_r;
+    }
+    v.total += reward;
+    // next_request (:1131-1163), prepared
+    v.dt = pr.dt;
+    v.t = pr.arr;
+    v.s1 = (v.s1 & ~((3u << S1_RZ) | (7u << S1_THR))) | (((pr.arz >> 12) & 3u) << S1_RZ) |
+           (((pr.arz >> 8) & 7u) << S1_THR);
+    img_request(me, v, em, E);
+    return reward;
+}
+
+// ---- the lean record: RO_REC_BYTES = 160 per env in the state blob's record area ----------
+//   words 0..7 emeta (em_pack) | 8,9 topo | 10,11 zcap | 12,13 nz0 | 14,15 nz1 | 16,17 x1 |
+//   18,19 x2 | 20 thr_idx | rz << 8 | 21..23 - | 24..39 lat0 (f64) of endpoints 0..7
+constexpr uint32_t LREC_LAT0 = 96;  // byte offset of lat0[0]
+
+// reset()'s draws for one env (the same map and owner rule as tpe_write_record), W lanes
+template <int W>
+__device__ __forceinline__ void lean_write_record(const Params& p, int64_t env, uint32_t episode, int lane) {
+    uint64_t zc = 0, nz0 = 0, nz1 = 0;
+    for (int w = 0; w < p.NZW; ++w) {  // nodes (:349-373)
+        uint64_t word = 0;
+        for (int n = 32 * w + lane; n < 32 * (w + 1) && n < p.N; n += W) {
+            int ty, zo, cpu;
+            node_draw<false>(p, env, episode, n, ty, zo, cpu);
+            zc += (uint64_t)node_cpu_int(ty) << (16 * zo);
+            word |= (uint64_t)zo << (2 * (n & 31));
+        }
+        word = slice_or64<W>(word);
+        if (w == 0) nz0 = word;
+        if (w == 1) nz1 = word;
+    }
+    zc = slice_sum64<W>(zc);
+    double lat0 = 0.0;  // endpoints (:328, :379-386)
+    int node = 0;
+    if (lane < p.E) {
+        const U4 d = draw(p, env, episode, (uint32_t)lane, D_EP);
+        lat0 = 1.0 + 99.0 * u53(d.x, d.y);
+        node = (int)bounded(d.z, 24);
+    }
+    int owner = lane;  // first endpoint hosted on the same node
+    for (int e2 = 0; e2 < p.E; ++e2) {
+        const int nd2 = (int)shfl_u32<W>((uint32_t)node, e2);
+        if (nd2 == node && e2 < owner) owner = e2;
+    }
+    uint32_t* out = reinterpret_cast<uint32_t*>(p.rec + env * (RO_REC_BYTES / 16));
+    if (lane < p.E) {
+        int ty, zo, cpu;
+        node_draw<false>(p, env, episode, node, ty, zo, cpu);
+        const uint64_t lb = (uint64_t)__double_as_longlong(lat0);
+        *reinterpret_cast<uint2*>(out + 24 + 2 * lane) = make_uint2((uint32_t)lb, (uint32_t)(lb >> 32));
+        out[lane] = em_pack(zo, owner, ty, cpu, node);
+    }
+    const uint64_t topo = scen_topo(p, env, episode);  // (:331-338)
+    double x1, x2;  // next_request() closing reset() (:397)
+    int r, n;
+    slice_request_draws<W, false>(p, env, episode, 0, lane, true, x1, x2, r, n);
+    if (lane == 0) {
+        const int rz = (int)(((n < 32 ? nz0 : nz1) >> (2 * (n & 31))) & 3);
+        const uint64_t w[6] = {topo, zc, nz0, nz1, (uint64_t)__double_as_longlong(x1),
+                               (uint64_t)__double_as_longlong(x2)};
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+            *reinterpret_cast<uint2*>(out + 8 + 2 * j) = make_uint2((uint32_t)w[j], (uint32_t)(w[j] >> 32));
+        out[20] = (uint32_t)((r + 6) % 7) | ((uint32_t)rz << 8);
+    }
+}
+
+// The next episodes of the envs in grp (<= 8 of them) from their records, staged (by the wave)
+// in each env's own image region, rebuilt in place by the wave: 8 lanes per env build its
+// endpoint rows (zone / capacity pair, initial cpu and latency) and its emeta register words
+// (lem), and each env's own lane ("mine") loads its scalars and the lem words.  Words of the
+// staged record: 0..7 emeta, 8..20 scalars, 24..39 lat0; the rows land on words 0..31 and the
+// lem words on 32..39, which the env's lane then overwrites with the reject row and the
+// request block (it reads them first).
+template <int ET, int RT>
+__device__ __forceinline__ void lean_restart_group(const Params& p, const LDims<ET, RT>& d, uint32_t* wimg,
+                                                   uint64_t grp, int lane, bool mine, LEnv& v,
+                                                   uint32_t (&em)[TPE_E], uint32_t (&ed)[TPE_E], uint32_t* me) {
+    // the scalars of each restarting env, by its own lane, before any row overwrites them
+    if (mine) {
+        const uint4* q = reinterpret_cast<const uint4*>(me);
+        const uint4 s0 = q[2], s1 = q[3], s2 = q[4];
+        const uint32_t s3 = me[20];
+        v.topo = (uint64_t)s0.x | ((uint64_t)s0.y << 32);
+        v.zcap = (uint64_t)s0.z | ((uint64_t)s0.w << 32);
+        v.nz0 = (uint64_t)s1.x | ((uint64_t)s1.y << 32);
+        v.nz1 = (uint64_t)s1.z | ((uint64_t)s1.w << 32);
+        const uint32_t episode = (uint32_t)(v.acc3 >> 32) + 1;
+        v.acc3 = (uint64_t)episode << 32;
+        v.acc2 = 0;
+        v.sum_lat = 0;
+        v.sum_cpu = 0;
+        v.sum_hi = 0;
+        v.total = 0.0;
+        v.last_r = p.init_last_r;
+        v.s0 = 0;  // step, acc
+        // intra 0, penalty 0, reset_done 1, bad kept (the status word)
+        v.s1 = (v.s1 & (1u << S1_BAD)) | (1u << S1_RD) | ((s3 & 7u) << S1_THR) | (((s3 >> 8) & 3u) << S1_RZ);
+        const double x1 = __longlong_as_double((long long)((uint64_t)s2.x | ((uint64_t)s2.y << 32)));
+        const double x2 = __longlong_as_double((long long)((uint64_t)s2.z | ((uint64_t)s2.w << 32)));
+        const double arrival = v.t + x1;
+        const double departure = arrival + x2;
+        v.dt = (float)(departure - arrival);
+        v.t = arrival;
+    }
+    // endpoint e of the g-th env of grp on lane 8 g + e
+    const int e = lane & 7, g = lane >> 3;
+    int el = -1;
+    {
+        uint64_t m = grp;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int b = m ? (int)__builtin_ctzll(m) : -1;
+            if (g == i) el = b;
+            m &= m - 1;
+        }
+    }
+    const bool helper = el >= 0 && e < ET;
+    uint32_t* ri = wimg + (el < 0 ? 0 : el) * IMG_W;
+    uint32_t mw = 0, l0lo = 0, l0hi = 0, zlo = 0, zhi = 0;
+    if (helper) {
+        mw = ri[e];
+        l0lo = ri[24 + 2 * e];
+        l0hi = ri[25 + 2 * e];
+        zlo = ri[10];
+        zhi = ri[11];
+    }
+    wave_lds_sync();  // (every read of the staged records is back before the first row is written)
+    if (helper) {
+        const double l0 = __longlong_as_double((long long)((uint64_t)l0lo | ((uint64_t)l0hi << 32)));
+        const int z = em_zone(mw);
+        const uint64_t zcap = (uint64_t)zlo | ((uint64_t)zhi << 32);
+        // (the row's topology word is written with the request block below)
+        *reinterpret_cast<uint4*>(ri + 4 * e) =
+            make_uint4(img_zc(z, zcap_val(zcap, z)), 0u, __float_as_uint((float)em_c0(mw)), __float_as_uint((float)l0));
+        ri[32 + e] = lem_make(mw, l0);  // table rows 0: the initial values
+    }
+    wave_lds_sync();
+    if (mine) {
+        const uint4 a = *reinterpret_cast<const uint4*>(me + 32), b = *reinterpret_cast<const uint4*>(me + 36);
+        const uint32_t lw[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int i = 0; i < TPE_E; ++i) {
+            em[i] = i < ET ? lw[i] : 0u;
+            ed[i] = 0u;
+        }
+        *reinterpret_cast<uint4*>(me + 4 * d.E) = make_uint4(IMG_ZC_REJECT, F32_M1, F32_M1, F32_M1);
+        img_request(me, v, em, d.E);
+    }
+}
+
+// lane -> (env, record chunk) of the record fetch: lanes 10 i .. 10 i + 9 fetch the record
+// of the i-th lowest env of m (i < 6); returns the env's lane or -1
+__device__ __forceinline__ int rec_fetch_env(uint64_t m, int lane, int& chunk) {
+    const int i = lane / 10;
+    chunk = lane - 10 * i;
+    int el = -1;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const int b = m ? (int)__builtin_ctzll(m) : -1;
+        if (i == j) el = b;
+        m &= m - 1;
+    }
+    return el;
+}
+constexpr int REC_FETCH_MAX = 6;
+
+// the ep_stats row (write_stats_row's values) as 8 paired 16-byte stores
+struct Acc {
+    double total;
+    uint64_t acc2, acc3, sum_lat, sum_cpu;
+    uint32_t sum_hi, s0, s1;
+};
+template <int ET>
+__device__ __forceinline__ void stats_row_store(Rsrc st, uint32_t voff, const Acc& a) {
+    static_assert(LB_ST_RETURN == 0 && LB_ST_LENGTH == 1 && LB_ST_ACCEPTED == 2 && LB_ST_SUM_LATENCY == 3 &&
+                      LB_ST_SUM_TOPOLOGY == 4 && LB_ST_SUM_TOPOLOGY_UPDATED == 5 && LB_ST_SUM_COST == 6 &&
+                      LB_ST_SUM_CPU == 7 && LB_ST_INTRA == 8 && LB_ST_INTER == 9 && LB_ST_GINI == 10 &&
+                      LB_ST_EPISODE == 11 && LB_ST_SUM_LATENCY_REM == 12 && LB_ST_SUM_CPU_REM == 13 &&
+                      LB_ST_SUM_TOPOLOGY_UPDATED_D == 14 && LB_ST_K == 16,
+                  "ep_stats column order");
+    const Scal s = sc_unpack((uint64_t)a.s0 | ((uint64_t)a.s1 << 32));
+    const uint32_t sum_topo = (uint32_t)a.acc2;
+    // one pair per store, computed next to it (all 16 values at once held 17 more registers)
+    auto put = [&](int i, double x, double y) {
+        const uint64_t lo = (uint64_t)__double_as_longlong(x), hi = (uint64_t)__double_as_longlong(y);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)},
+                                               st, voff + 16u * i, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    double ls, lr, cs, cr;
+    put(0, a.total, (double)s.step);
+    xsum_pair(a.sum_lat, a.sum_hi & 0x7Fu, ls, lr);
+    put(1, (double)s.acc, ls);
+    put(2, (double)sum_topo, (double)s.intra + 1.7 * (double)(sum_topo - (uint32_t)s.intra));
+    xsum_pair(a.sum_cpu, (a.sum_hi >> XH_CPU) & 0x1Fu, cs, cr);
+    put(3, (double)(uint32_t)a.acc3, cs);
+    put(4, (double)s.intra, (double)(s.acc - s.intra));
+    put(5, gini_of(a.acc2, s.acc, ET), (double)(uint32_t)(a.acc3 >> 32));
+    put(6, lr, cr);
+    put(7, (double)((int32_t)a.sum_hi >> XH_D), 0.0);
+}
+
+// one group of terminal observations: lane l reads piece l % P of env l / P of the group
+// (the (l / P)-th lowest set bit of m), or -1 / nothing for lanes past the group
+template <int P>
+__device__ __forceinline__ int term_group_env(uint64_t m, int lane) {
+    constexpr int G = 64 / P;
+    const int g = lane / P;
+    int el = -1;
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+        const int b = m ? (int)__builtin_ctzll(m) : -1;
+        if (g == i) el = b;
+        m &= m - 1;
+    }
+    return el;
+}
+template <int P>
+__device__ __forceinline__ uint64_t drop_low(uint64_t m) {  // m without its G = 64 / P lowest bits
+#pragma unroll
+    for (int i = 0; i < 64 / P; ++i) m &= m - 1;
+    return m;
+}
+__device__ __forceinline__ float4 term_piece(const uint32_t* wimg, int el, int pc) {
+    const char* base = reinterpret_cast<const char*>(wimg) + el * (IMG_W * 4);
+    const uint4 A = *reinterpret_cast<const uint4*>(base + 16 * (pc >> 1));
+    const uint4 S = *reinterpret_cast<const uint4*>(base + 4 * IMG_S);
+    return img_piece(A, S, (pc & 1) != 0);
+}
+
+template <int KIND, int ET, int RT, int NZW, bool NAIVE, bool ACT>
+__global__ __launch_bounds__(256, 4) void k_rollout_lean(Params p, int K, int32_t* act_out) {
+    constexpr int NB = 256, NW = NB / 64, P = 2 * RT, GT = 64 / P;
+    constexpr int FAST = GT < REC_FETCH_MAX ? GT : REC_FETCH_MAX;  // restarts per step of the fast path
+    static_assert(ET >= 1 && ET <= TPE_E && (RT == ET || RT == ET + 1), "compile-time geometry");
+    __shared__ __attribute__((aligned(16))) uint32_t simg[NW][64 * IMG_W];
+    const LDims<ET, RT> d(p);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t* wimg = simg[wv];
+    uint32_t* me = wimg + lane * IMG_W;
+    // whole waves only (the host checks B % 64 == 0): every lane of a live wave is a live env,
+    // and the waves past B in a partial last block leave (no block barrier follows: every
+    // synchronisation below is within the wave)
+    const int64_t env0 = (int64_t)blockIdx.x * NB + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63);
+    if (env0 >= p.B) return;
+    const int64_t env = env0 + lane;
+    const uint32_t envi = (uint32_t)env;
+    const Rsrc blob = rsrc_of(p.lat_lut);  // tables, lat0 array and records (blob < 4 GiB: host check)
+    const uint32_t rec_off = (uint32_t)(reinterpret_cast<const char*>(p.rec) - reinterpret_cast<const char*>(p.lat_lut));
+    const uint32_t cpu0 = (uint32_t)(reinterpret_cast<const char*>(p.cpu_lut) - reinterpret_cast<const char*>(p.lat_lut));
+
+    // the next episodes of the envs that end inside the launch, into their records
+    {
+        const int to_done = p.L - (int)(p.sc[env] & 0xFFFF);
+        const bool fin = to_done >= 1 && to_done <= K;
+        const uint64_t fm = __ballot(fin);
+        if (fin) {
+            uint32_t* it = wimg + 2 * __popcll(fm & ((1ull << lane) - 1));
+            it[0] = (uint32_t)lane;
+            it[1] = (uint32_t)(p.acc3[env] >> 32) + 1;
+        }
+        wave_lds_sync();
+        const int nf = __popcll(fm), g = lane / RS_W, gl = lane % RS_W;
+        for (int r0 = 0; r0 < nf; r0 += 64 / RS_W) {
+            const int i = r0 + g;
+            if (i < nf) lean_write_record<RS_W>(p, env0 + (int64_t)wimg[2 * i], wimg[2 * i + 1], gl);
+        }
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+
+    LEnv v;
+    uint32_t em[TPE_E], ed[TPE_E];
+    {
+        float olat[TPE_E], ocpu[TPE_E];
+#pragma unroll
+        for (int e = 0; e < TPE_E; ++e) {
+            em[e] = 0u;
+            ed[e] = 0u;
+            olat[e] = 0.f;
+            ocpu[e] = 0.f;
+            if (e < ET) {
+                const int64_t i = (int64_t)e * p.B + env;
+                const double l0 = p.lat0[i];
+                const uint32_t m = p.emeta[i];
+                ed[e] = p.edyn[i];
+                em[e] = lem_make(m, l0);
+                olat[e] = (float)lat_of(p, l0, ed[e]);
+                ocpu[e] = (float)cpu_of(p, m, ed[e]);
+            }
+        }
+        v.t = p.t[env];
+        const uint64_t sc = p.sc[env];
+        v.s0 = (uint32_t)sc;
+        v.s1 = (uint32_t)(sc >> 32);
+        v.zcap = p.zcap[env];
+        v.acc2 = p.acc2[env];
+        v.acc3 = p.acc3[env];
+        v.topo = p.topo[env];
+        v.nz0 = p.nzone[env];
+        v.nz1 = NZW > 1 ? p.nzone[p.B + env] : 0;
+        v.sum_lat = p.sum_lat[env];
+        v.sum_cpu = p.sum_cpu[env];
+        v.sum_hi = p.sum_hi[env];
+        v.total = p.total[env];
+        v.last_r = NAIVE ? 0.0 : p.last_r[env];
+        v.dt = 0.f;
+        img_endpoints(me, d, em, v.zcap, olat, ocpu);
+    }
+
+    bool new_episode = false;
+    uint32_t l0off = (uint32_t)(reinterpret_cast<const char*>(p.lat0) - reinterpret_cast<const char*>(p.lat_lut)) +
+                     envi * 8u;
+    uint32_t l0step = (uint32_t)p.B * 8u;
+    const uint32_t obs_wave = (uint32_t)(env0 * P * 16);  // byte offset of the wave's obs block in a slot
+
+    // record prefetch of the envs that end at the next step (<= FAST of them: else the slow
+    // path in the loop fetches them itself)
+    uint4 qn = make_uint4(0u, 0u, 0u, 0u);
+    auto fetch_next = [&](int steps_done) {
+        const uint64_t mn = __ballot((int)(steps_done + 1) == p.L);
+        if (mn && __popcll(mn) <= FAST) {
+            int chunk;
+            const int el = rec_fetch_env(mn, lane, chunk);
+            if (el >= 0) qn = buf_ld_u128(blob, rec_off + (uint32_t)(env0 + el) * RO_REC_BYTES + 16u * chunk);
+        }
+    };
+
+    LPrepL pr;
+    auto prep = [&](auto&& between) {
+        // the next step's action, its endpoint's 4 table gathers, the record prefetch, then the
+        // request draws with the previous step's stores spread over between(0..5)
+        LPrepL r;
+        TEnv tv;
+        tv.topo = v.topo;
+        tv.zcap = v.zcap;
+        tv.acc3 = v.acc3;
+        tv.s.rz = (int)((v.s1 >> S1_RZ) & 3);
+        const int step = (int)(v.s0 & 0xFFFF);
+        tv.s.step = step;
+        const int a = lean_policy<KIND>(p, env, tv, em, ed);
+        const bool accept = a < ET;
+        const int ai = accept ? a : 0;
+        const uint32_t emA = pick8(em, ai), edA = pick8(ed, ai);
+        const int oA = em_owner(emA);
+        const uint32_t edO = pick8(ed, oA);
+        const int jA = ed_j(edA);
+        const int Mn = ed_M(edO) < CMAX ? ed_M(edO) + 1 : CMAX;
+        const int jn = jA < CMAX ? jA + 1 : CMAX;
+        const int k0A = lem_k0(emA), c0A = em_c0(emA);
+        // selected_endpoint_latency: lat0 on a first selection (LAT row 0 holds trunc(lat0))
+        r.sel_lat = buf_ld_f64(blob, jA == 0 ? l0off + (uint32_t)ai * l0step : (uint32_t)(jA * LAT_ROWS + k0A) * 8u);
+        r.sel_cpu = buf_ld_f64(blob, cpu0 + (uint32_t)(ed_m(edA) * CPU_ROWS + c0A) * 8u);
+        r.next_lat = buf_ld_f64(blob, (uint32_t)(jn * LAT_ROWS + k0A) * 8u);
+        r.next_cpu = buf_ld_f64(blob, cpu0 + (uint32_t)(Mn * CPU_ROWS + c0A) * 8u);
+#ifndef LB_LEAN_NO_PREF
+        fetch_next(step);
+#endif
+        // (each stage's stores are pinned between computed values: "memory" barriers that
+        // name the values just computed, so neither the compiler's IR passes nor its
+        // scheduler can bunch the stores or sink the computation past them)
+        asm volatile("" ::: "memory");
+        between(0);
+        asm volatile("" ::: "memory");
+        const uint32_t episode = (uint32_t)(v.acc3 >> 32), slot = (uint32_t)(step + 1);
+        const U4 wx = draw_o(p, env, episode, slot, D_REQ_X);
+        asm volatile("" ::"v"(wx.x), "v"(wx.y), "v"(wx.z), "v"(wx.w) : "memory");
+        between(1);
+        asm volatile("" ::: "memory");
+        const double x1 = p.inv_rate * std_exp(wx.x, wx.y);
+        asm volatile("" ::"v"(x1) : "memory");
+        between(2);
+        asm volatile("" ::: "memory");
+        const double x2 = p.call * std_exp(wx.z, wx.w);
+        // next_request()'s clock (:1135-1139): the same operations as at the step
+        r.arr = v.t + x1;
+        r.dt = (float)((r.arr + x2) - r.arr);
+        asm volatile("" ::"v"(r.arr), "v"(r.dt) : "memory");
+        between(3);
+        asm volatile("" ::: "memory");
+        const U4 wi = draw_o(p, env, episode, slot, D_REQ_I);
+        const int rr = (int)bounded(wi.x, 7), n = (int)bounded(wi.y, (uint32_t)p.N);
+        const uint64_t word = (NZW > 1 && n >= 32) ? v.nz1 : v.nz0;
+        const uint32_t rz = (uint32_t)((word >> (2 * (n & 31))) & 3);
+        r.arz = (uint32_t)a | ((uint32_t)((rr + 6) % 7) << 8) | (rz << 12);
+        asm volatile("" ::"v"(r.arz) : "memory");
+        between(4);
+        asm volatile("" ::: "memory");
+        between(5);
+        return r;
+    };
+    pr = prep([](int) {});
+
+    // one step (k): apply, auto-reset, then step k + 1's preparation with step k's stores
+    auto iter = [&](const int k) {
+        // issue priority by progress (k_rollout_img): a wave behind the others goes first
+        {
+            const int pl = 3 - (4 * k) / K;
+            if (pl >= 3) __builtin_amdgcn_s_setprio(3);
+            else if (pl == 2) __builtin_amdgcn_s_setprio(2);
+            else if (pl == 1) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+        // every load of the last preparation is consumed here, on every path: its wait is one
+        // counted vmcnt at this point (a value left pending on some path -- a reject never reads
+        // the next latency -- made the compiler drain the whole queue where the register was
+        // next rewritten)
+        asm volatile("" ::"v"(pr.sel_lat), "v"(pr.sel_cpu), "v"(pr.next_lat), "v"(pr.next_cpu), "v"(qn.x), "v"(qn.y),
+                     "v"(qn.z), "v"(qn.w));
+        const int a_k = (int)(pr.arz & 0xFFu);
+        v.s0 += 1;  // step (<= L: the episode ends there)
+        const bool done = (int)(v.s0 & 0xFFFF) == p.L;  // (:472)
+        const double reward = lean_apply_l<ET, RT, NAIVE ? (int)LB_REWARD_NAIVE : -1>(p, pr, v, em, ed, me);
+        const uint64_t m = __ballot(done);
+        if (m) {  // VecEnv auto-reset: episode stats + terminal obs, then the record's episode
+            // (the stores below are younger than the prefetched record, so waiting for it does
+            // not wait for them; the next gathers do, but a few 16-byte stores issued just
+            // before them cost about nothing next to the gathers' own round trip)
+            if (done) stats_row_store<ET>(rsrc_of(p.ep_stats), envi * (uint32_t)(8 * LB_ST_K),
+                                      Acc{v.total, v.acc2, v.acc3, v.sum_lat, v.sum_cpu, v.sum_hi, v.s0, v.s1});
+            wave_lds_sync();  // (apply's image writes, read by other lanes below)
+            // groups of up to FAST ending envs: their terminal observations (one store), their
+            // records into their image regions (prefetched when the whole step is one group,
+            // else loaded here: a block of its own, so the wait for the prefetched record stays
+            // a counted vmcnt instead of a vmcnt(0) behind the stores above), the restarts in place
+            const int pc = lane % P;
+            bool pre = __popcll(m) <= FAST;
+            for (uint64_t mm = m; mm;) {  // (wave-uniform)
+                uint64_t grp = mm;
+#pragma unroll
+                for (int j = 0; j < FAST; ++j) mm &= mm - 1;
+                grp &= ~mm;
+                const int tel = term_group_env<P>(grp, lane);
+                if (tel >= 0)
+                    buf_st_f4<BUF_NT>(term_piece(wimg, tel, pc), rsrc_of(p.term_obs),
+                                      (uint32_t)((env0 + tel) * P + pc) * 16u, 0);
+                int chunk;
+                const int rl = rec_fetch_env(grp, lane, chunk);
+                uint4* dst = reinterpret_cast<uint4*>(wimg + rl * IMG_W + 4 * chunk);
+                wave_lds_sync();  // (the terminal pieces are read before the records overwrite them)
+                if (pre) {
+                    if (rl >= 0) *dst = qn;
+                } else {
+                    if (rl >= 0) *dst = buf_ld_u128(blob, rec_off + (uint32_t)(env0 + rl) * RO_REC_BYTES + 16u * chunk);
+                }
+                wave_lds_sync();
+                const bool mine = done && ((grp >> lane) & 1);
+                lean_restart_group(p, d, wimg, grp, lane, mine, v, em, ed, me);
+                if (mine) {
+                    new_episode = true;
+                    l0off = rec_off + envi * RO_REC_BYTES + LREC_LAT0;
+                    l0step = 8u;
+                }
+                pre = false;
+            }
+        }
+        // step k's outputs leave after step k + 1's gathers, spread over its request draws
+        const Rsrc out = rsrc_of(p.obs + k * (int64_t)p.B * RT * 8);
+        const Rsrc rw = rsrc_of(p.reward + (int64_t)k * p.B), dn = rsrc_of(p.done + (int64_t)k * p.B);
+        wave_lds_sync();
+        ImgCursor cur = img_cursor(d, lane);
+        const bool h = (lane & 1) != 0;
+        auto stores = [&](int stage) {
+            if (stage == 0) {
+                if (ACT) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)a_k, rsrc_of(act_out + (int64_t)k * p.B),
+                                                               envi * 4u, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)reward), rw, envi * 4u, 0, BUF_NT);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)done, dn, envi, 0, BUF_NT);
+            }
+            constexpr int per = (P + PREP_STAGES - 1) / PREP_STAGES;
+            // (the scalar offsets from an opaque copy of the wave's base: hoisted out of the
+            // step loop they were 2R SGPRs, spilled and read back with v_readlane per store)
+            uint32_t so = obs_wave + 1024u * (uint32_t)(stage * per);
+            asm volatile("" : "+s"(so));
+#pragma unroll
+            for (int it = stage * per; it < (stage + 1) * per && it < P; ++it) {
+                buf_st_f4<BUF_NT>(img_read_piece(wimg, cur, h), out, (uint32_t)lane * 16u,
+                                  so + 1024u * (uint32_t)(it - stage * per));
+                img_advance(d, cur);
+            }
+        };
+        if (k + 1 < K) {
+            pr = prep(stores);
+        } else {
+            for (int s = 0; s < PREP_STAGES; ++s) stores(s);
+        }
+        wave_lds_sync();  // (the next step rewrites the image)
+    };
+    // (the first step is peeled off the loop: the loop is then entered, like its back edge,
+    // with the gathers followed by a step's stores in flight, and the compiler's wait for
+    // the gathers is a counted vmcnt instead of the vmcnt(0) the loop entry's shape forced)
+    if (K > 0) iter(0);
+    for (int k = 1; k < K; ++k) iter(k);
+    // (the write-back's addresses from an opaque copy of the env index: the compiler would
+    // otherwise keep the launch start's 64-bit addresses alive across the loop)
+    int64_t ew = env;
+    asm volatile("" : "+v"(ew));
+#pragma unroll
+    for (int e = 0; e < TPE_E; ++e)
+        if (e < ET) p.edyn[(int64_t)e * p.B + ew] = ed[e];
+    if (new_episode) {  // the scenario of the episode started in the launch, from its record
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(p.rec + ew * (RO_REC_BYTES / 16));
+#pragma unroll
+        for (int e = 0; e < TPE_E; ++e) {
+            if (e >= ET) continue;
+            const int64_t i = (int64_t)e * p.B + ew;
+            p.lat0[i] = __longlong_as_double((long long)((uint64_t)w[24 + 2 * e] | ((uint64_t)w[25 + 2 * e] << 32)));
+            p.emeta[i] = w[e];
+        }
+        p.topo[ew] = v.topo;
+        p.zcap[ew] = (uint64_t)w[10] | ((uint64_t)w[11] << 32);
+        p.nzone[ew] = v.nz0;
+        if (NZW > 1) p.nzone[p.B + ew] = v.nz1;
+    }
+    p.t[ew] = v.t;
+    p.sc[ew] = (uint64_t)v.s0 | ((uint64_t)v.s1 << 32);
+    p.acc2[ew] = v.acc2;
+    p.acc3[ew] = v.acc3;
+    p.sum_lat[ew] = v.sum_lat;
+    p.sum_cpu[ew] = v.sum_cpu;
+    p.sum_hi[ew] = v.sum_hi;
+    p.total[ew] = v.total;
+    if (!NAIVE) p.last_r[ew] = v.last_r;
+}
+
+}  // namespace lbk

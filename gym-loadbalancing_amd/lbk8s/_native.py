@@ -10,11 +10,19 @@ import ctypes as C
 import os
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblbk8s.so")
-ABI_VERSION = 7
+_PRODUCT_LIB = LIB_PATH
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+# csrc/Makefile's SRCS, in order: the library embeds the SHA-256 of their concatenation
+SOURCES = ("lbk8s.hip", "lbk8s_common.h", "lbk8s_slice.h", "lbk8s_tpe.h", "lbk8s_rollout.h", "lbk8s_lean.h",
+           "lbk8s_deepsets.h", "lbk8s_ds_train.h", "../../include/lbk8s.h")
+ABI_VERSION = 8
 
 LB_REWARD = {"naive": 0, "latency": 1, "fairness": 2, "multi": 3}
 LB_RNG_PHILOX, LB_RNG_TRACE = 0, 1
 LB_POLICY = {"topo": 0, "zone_cpu": 1, "endpoint_cpu": 2, "random": 3}
+# lb_rollout_kernel's answers (include/lbk8s.h LB_ROLLOUT_*)
+LB_ROLLOUT = {0: "k_rollout_lean", 1: "k_rollout_img", 2: "k_rollout_tpe", 3: "policy+step launches",
+              4: "k_rollout_slice"}
 LB_FIELD = {"endpoint_latency": 0, "endpoint_cpu_usage_percentage": 1,
             "endpoint_topology_latency": 2, "endpoint_zone_cpu_capacity": 3, "endpoint_zone": 4,
             "endpoint_node": 5, "avg_load_served": 6, "current_time": 7, "current_step": 8,
@@ -81,6 +89,50 @@ class NativeLibraryMissing(RuntimeError):
     pass
 
 
+class StaleNativeLibrary(RuntimeError):
+    pass
+
+
+class _Tolerant:
+    """A diagnostic library of another ABI: symbols it lacks become no-op stand-ins, so
+    setting their argtypes does not fail (calling one raises)."""
+
+    class _Missing:
+        def __init__(self, name):
+            self.name = name
+
+        def __call__(self, *a):
+            raise AttributeError(f"diagnostic library lacks {self.name}")
+
+    def __init__(self, L):
+        self.__dict__["_L"] = L
+
+    def __getattr__(self, name):
+        try:
+            return getattr(self._L, name)
+        except AttributeError:
+            m = _Tolerant._Missing(name)
+            self.__dict__[name] = m
+            return m
+
+    def __setattr__(self, name, value):
+        setattr(self._L, name, value)
+
+
+def source_hash():
+    """First 16 hex digits of the SHA-256 of the library's sources (csrc/Makefile's SRC_HASH),
+    or None where the sources are absent."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in SOURCES:
+        path = os.path.normpath(os.path.join(CSRC, f))
+        if not os.path.exists(path):
+            return None
+        with open(path, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def lib():
     """Load liblbk8s.so (once). Raises NativeLibraryMissing if it was not built."""
     global _lib
@@ -92,6 +144,9 @@ def lib():
             f"{LIB_PATH} not found: build it with `make -C gym-loadbalancing_amd/csrc` "
             "(or __graft_entry__.build()); there is no CPU fallback")
     L = C.CDLL(LIB_PATH)
+    product = os.path.abspath(LIB_PATH) == _PRODUCT_LIB
+    if not product:  # a diagnostic build (tools/ A/B runs): an older ABI may lack symbols
+        L = _Tolerant(L)
     vp, i64, i32 = C.c_void_p, C.c_int64, C.c_int32
     cfgp = C.POINTER(LBConfigC)
     trp = C.POINTER(LBTraceC)
@@ -104,6 +159,7 @@ def lib():
     L.lb_step.argtypes = [vp, cfgp, i64, vp, vp, vp, vp, vp, vp, trp, vp]
     L.lb_policy.argtypes = [vp, cfgp, i64, i32, vp, vp]
     L.lb_rollout.argtypes = [vp, cfgp, i64, i32, i32, vp, vp, vp, vp, vp, vp, vp]
+    L.lb_rollout_kernel.argtypes = [cfgp, i64, i32, i32, C.POINTER(C.c_int32)]
     L.lb_get_field.argtypes = [vp, cfgp, i64, i32, vp, vp]
     L.lb_get_stats.argtypes = [vp, cfgp, i64, vp, vp]
     L.lb_status.argtypes = [vp, cfgp, i64, vp, vp]
@@ -122,14 +178,21 @@ def lib():
     L.lb_replay_sample.argtypes = [i64, i32, i64, i32, C.c_uint64] + [vp] * 12 + [vp]
     L.lb_ds_set_grads.argtypes = [vp, vp, vp, i64, i32, vp, vp]
     for f in ("lb_validate_config", "lb_state_bytes", "lb_init", "lb_reset", "lb_step", "lb_policy", "lb_rollout",
+              "lb_rollout_kernel",
               "lb_get_field", "lb_get_stats", "lb_status", "lb_ds_pack", "lb_ds_forward",
               "lb_ds_train_forward", "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax",
               "lb_replay_add", "lb_ppo_head", "lb_episode_log", "lb_dqn_act", "lb_dqn_head",
               "lb_replay_sample", "lb_ds_set_grads"):
         getattr(L, f).restype = C.c_int
     v = L.lb_abi_version()
-    if v != ABI_VERSION:
+    if v != ABI_VERSION and product:
         raise RuntimeError(f"liblbk8s.so ABI {v} != expected {ABI_VERSION}; rebuild it")
+    if product:  # (another LIB_PATH: a diagnostic build of other sources, tools/ only)
+        L.lb_source_hash.restype = C.c_char_p
+        built, now = L.lb_source_hash().decode(), source_hash()
+        if now is not None and built != now:
+            raise StaleNativeLibrary(f"{LIB_PATH} was built from sources {built}, the tree's are {now}: "
+                                     "rebuild it (make -C gym-loadbalancing_amd/csrc, or __graft_entry__.build())")
     _lib = L
     return L
 
@@ -148,4 +211,5 @@ EXPORTED_SYMBOLS = ("lb_abi_version", "lb_last_error", "lb_validate_config", "lb
                     "lb_init", "lb_reset", "lb_step", "lb_policy", "lb_rollout", "lb_get_field", "lb_get_stats",
                     "lb_status", "lb_ds_pack", "lb_ds_forward", "lb_ds_train_forward",
                     "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax", "lb_replay_add", "lb_ppo_head",
-                    "lb_episode_log", "lb_dqn_act", "lb_dqn_head", "lb_replay_sample", "lb_ds_set_grads")
+                    "lb_episode_log", "lb_dqn_act", "lb_dqn_head", "lb_replay_sample", "lb_ds_set_grads",
+                    "lb_rollout_kernel", "lb_source_hash")

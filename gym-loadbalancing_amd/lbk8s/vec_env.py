@@ -455,6 +455,14 @@ class LBVecEnv:
             self._ptr(terminal_obs_out if terminal_obs_out is not None else self.terminal_obs),
             self._ptr(ep_stats_out if ep_stats_out is not None else self.ep_stats), self._stream()))
 
+    def rollout_kernel(self, steps, outputs_all=True):
+        """The kernel lb_rollout launches for `steps` vector steps with every output given
+        (outputs_all) or not (lb_rollout_kernel; host only)."""
+        k = C.c_int32(-1)
+        _native.check(self._L.lb_rollout_kernel(C.byref(self._c), self.num_envs, int(steps), int(bool(outputs_all)),
+                                                C.byref(k)))
+        return _native.LB_ROLLOUT[k.value]
+
     def policy(self, kind, out=None):
         """Batched envs/baselines.py greedy policy or uniform random -> (B,) int32 device tensor."""
         out = out if out is not None else self.torch.empty(self.num_envs, dtype=self.torch.int32,

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LBK8S_ABI_VERSION 7
+#define LBK8S_ABI_VERSION 8
 
 /* reward_function names of loadbalancer_k8s_env.py:20-31 */
 enum { LB_REWARD_NAIVE = 0, LB_REWARD_LATENCY = 1, LB_REWARD_FAIRNESS = 2, LB_REWARD_MULTI = 3 };
@@ -138,6 +138,10 @@ typedef struct lb_trace {
 
 int lb_abi_version(void);
 const char* lb_last_error(void);
+/* Build provenance: the first 16 hex digits of the SHA-256 of the library's sources (the
+ * Makefile's SRCS, concatenated in order) it was compiled from; the host side refuses a
+ * library whose sources have changed since (a stale build). */
+const char* lb_source_hash(void);
 
 /* Validate a configuration (reference constructor constraints). 0 = ok. */
 int lb_validate_config(const lb_config* cfg);
@@ -182,6 +186,20 @@ int lb_step(void* state, const lb_config* cfg, int64_t num_envs, const int32_t* 
 int lb_rollout(void* state, const lb_config* cfg, int64_t num_envs, int32_t policy, int32_t steps,
                float* obs_out, float* reward_out, uint8_t* done_out, int32_t* actions_out,
                float* terminal_obs_out, double* ep_stats_out, void* stream);
+
+/* Which kernel lb_rollout launches for (cfg, num_envs, steps), with every output pointer
+ * non-NULL (outputs_all != 0) or not: host only, no device call (ABI 8).
+ *   LB_ROLLOUT_LEAN   k_rollout_lean: thread-per-env, E = 8 / R = 9 (N <= 32) or E = 6 /
+ *                     R = 7 (N <= 64), L >= K, B % 64 == 0, B > 65,536, all outputs
+ *   LB_ROLLOUT_IMG    k_rollout_img: thread-per-env, L >= K
+ *   LB_ROLLOUT_TPE    k_rollout_tpe (64-bit offsets; also L < K or no auto-reset)
+ *   LB_ROLLOUT_STEPS  K policy + step launches (thread-per-env, N > 64)
+ *   LB_ROLLOUT_SLICE  k_rollout_slice
+ * The LEAN / IMG kernels address with 32-bit byte offsets from scalar bases; above 4 GiB of
+ * state (or of ep_stats rows, or of one obs slot for LEAN) lb_rollout takes LB_ROLLOUT_TPE. */
+enum { LB_ROLLOUT_LEAN = 0, LB_ROLLOUT_IMG = 1, LB_ROLLOUT_TPE = 2, LB_ROLLOUT_STEPS = 3, LB_ROLLOUT_SLICE = 4 };
+int lb_rollout_kernel(const lb_config* cfg, int64_t num_envs, int32_t steps, int32_t outputs_all,
+                      int32_t* kernel_out);
 
 /* Batched envs/baselines.py policies (and uniform random) on the current state. */
 int lb_policy(const void* state, const lb_config* cfg, int64_t num_envs, int32_t kind,

@@ -129,3 +129,64 @@ def test_host_asan_ubsan_abi():
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     assert "abi_asan: ok" in r.stdout
     assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
+
+
+def _rollout_kernel(B, steps, outputs_all=True, **kw):
+    from lbk8s import LBConfig, _native
+    L = _native.lib()
+    to_c = {k: kw.pop(k) for k in ("geometry", "auto_reset") if k in kw}
+    c = LBConfig(**kw).to_c(**to_c)
+    k = C.c_int32(-1)
+    assert L.lb_rollout_kernel(C.byref(c), B, steps, int(outputs_all), C.byref(k)) == 0, L.lb_last_error()
+    return _native.LB_ROLLOUT[k.value]
+
+
+def test_rollout_kernel_choice():
+    """lb_rollout_kernel (host only): the bench's launch takes k_rollout_lean; shapes it does
+    not cover fall back to k_rollout_img / k_rollout_tpe / the slice kernel."""
+    assert _rollout_kernel(1 << 20, 20) == "k_rollout_lean"                       # the driver's launch
+    assert _rollout_kernel(1 << 20, 100) == "k_rollout_lean"
+    assert _rollout_kernel(2000 * 64, 100, num_endpoints=6, num_nodes=48, num_zones=12) == "k_rollout_lean"
+    assert _rollout_kernel(1 << 20, 20, outputs_all=False) == "k_rollout_img"     # an output not written
+    assert _rollout_kernel((1 << 20) + 1, 20) == "k_rollout_img"                  # a partial last wave
+    assert _rollout_kernel(40000, 20, geometry="tpe") == "k_rollout_img"          # 64-thread blocks
+    assert _rollout_kernel(1 << 20, 20, num_endpoints=7) == "k_rollout_img"       # E without a lean build
+    assert _rollout_kernel(1 << 20, 20, reward_function="multi") == "k_rollout_lean"
+    assert _rollout_kernel(1 << 20, 120) == "k_rollout_tpe"                       # K > L: in-loop resets
+    assert _rollout_kernel(1 << 20, 20, auto_reset=False) == "k_rollout_tpe"
+    assert _rollout_kernel(1 << 20, 20, num_nodes=100) == "policy+step launches"
+    assert _rollout_kernel(4096, 20) == "k_rollout_slice"
+
+
+def test_rollout_32bit_offsets_guard():
+    """k_rollout_lean / k_rollout_img address with 32-bit byte offsets from scalar bases: a
+    launch whose state blob, ep_stats rows or obs slot would pass 4 GiB takes the 64-bit
+    k_rollout_tpe instead (an unguarded offset would wrap past 2^24 envs)."""
+    from lbk8s import LBConfig, _native
+    L = _native.lib()
+    c = LBConfig().to_c()
+    n = C.c_uint64()
+    # the largest whole-wave B whose blob and obs slot stay below 4 GiB takes the lean kernel
+    lo, hi = 1 << 16, 1 << 26
+    while hi - lo > 64:
+        mid = (lo + hi) // 2 // 64 * 64
+        assert L.lb_state_bytes(C.byref(c), mid, C.byref(n)) == 0
+        fits = n.value <= 0xFFFFFFFF and mid * 9 * 32 <= 0xFFFFFFFF and mid * 16 * 8 <= 0xFFFFFFFF
+        lo, hi = (mid, hi) if fits else (lo, mid)
+    assert _rollout_kernel(lo, 20) == "k_rollout_lean"
+    big = lo + 64 * 4096
+    assert _rollout_kernel(big, 20) == "k_rollout_tpe"
+    assert _rollout_kernel(1 << 24, 20) == "k_rollout_tpe"       # 2^24 envs: ~6.6 GB of state
+    assert _rollout_kernel((1 << 24) + 1, 20) == "k_rollout_tpe"
+
+
+def test_library_built_from_tree_sources():
+    """Build provenance: the in-tree liblbk8s.so embeds the SHA-256 of the sources it was
+    compiled from (csrc/Makefile SRC_HASH), equal to the tree's; and the Makefile hashes the
+    same files, in the same order, as the loader."""
+    from lbk8s import _native
+    L = _native.lib()
+    assert L.lb_source_hash().decode() == _native.source_hash()
+    mk = open(os.path.join(REPO, "gym-loadbalancing_amd", "csrc", "Makefile")).read()
+    srcs = re.search(r"^SRCS := (.*?)(?<!\\)$", mk, re.S | re.M).group(1).replace("\\\n", " ").split()
+    assert tuple(srcs) == _native.SOURCES

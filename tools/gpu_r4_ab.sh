@@ -14,7 +14,7 @@ OUT=gpurun_out/abroll.jsonl
 : > $OUT
 for rep in ${REPS:-1 2 3}; do
   for lib in ${LIBS}; do
-    timeout -k 10 150 python3 tools/roll_variants.py --lib $lib --variants 0 --reps 1 --steps ${STEPS:-100,20} ${ABARGS} \
+    timeout -k 10 150 python3 tools/roll_variants.py --lib $lib --variants ${VARIANTS:-0} --reps 1 --steps ${STEPS:-100,20} ${ABARGS} \
         >> $OUT 2> gpurun_out/abroll_err.log || { cat gpurun_out/abroll_err.log; exit 1; }
   done
 done
@@ -23,7 +23,7 @@ import json, collections
 rows = [json.loads(l) for l in open("gpurun_out/abroll.jsonl")]
 agg = collections.defaultdict(list)
 for r in rows:
-    agg[(r["lib"], r["K"])].append(r["us_per_step"])
+    agg[(r["lib"], r["variant"], r["K"])].append(r["us_per_step"])
 for k, v in sorted(agg.items()):
     print(k, v, "min", min(v))
 PY

@@ -3,9 +3,9 @@
 
     python tools/roll_variants.py [--envs N] [--steps K ...] [--variants 0,3] [--reps 3]
 
-Variants are selected in the product library with the experiment switch
-lbx_set_rollout_variant (0 the product dispatch, k_rollout_img; 3 the round-2
-k_rollout_tpe).  The env is staggered as in bench.py (1/L of the envs finish every
+Variants are selected with the experiment switch lbx_set_rollout_variant, which only a
+build with -DLB_EXPERIMENTS exports (0 the product dispatch, k_rollout_lean; 1
+k_rollout_img; 3 the round-2 k_rollout_tpe); the product library runs variant 0 only.  The env is staggered as in bench.py (1/L of the envs finish every
 step); each measurement is ONE HIP-event pair around `launches` back-to-back K-step launches
 into the obs ring.  Prints one JSON line per (rep, K, variant).
 """
@@ -17,6 +17,13 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "gym-loadbalancing_amd")]
+
+
+def _kernel_name(env, K):
+    try:
+        return env.rollout_kernel(K)
+    except AttributeError:  # a diagnostic library from before lb_rollout_kernel
+        return None
 
 
 def main():
@@ -42,7 +49,13 @@ def main():
     if args.lib:
         _native.LIB_PATH = os.path.abspath(args.lib)
     L = _native.lib()
-    L.lbx_set_rollout_variant.argtypes = [C.c_int]
+    if hasattr(L, "lbx_set_rollout_variant"):
+        L.lbx_set_rollout_variant.argtypes = [C.c_int]
+        set_variant = L.lbx_set_rollout_variant
+    else:
+        def set_variant(v):
+            if v != 0:
+                raise SystemExit(f"{_native.LIB_PATH} has no experiment switch: variant 0 only")
     staggers = [None]
     dev = torch.device("cuda", 0)
     B = args.envs
@@ -65,7 +78,7 @@ def main():
     for rep in range(args.reps):
         for K in [int(x) for x in args.steps.split(",")]:
             for var, stg in [(v, g) for v in [int(x) for x in args.variants.split(",")] for g in staggers]:
-                L.lbx_set_rollout_variant(var)
+                set_variant(var)
                 if args.lockstep:
                     env.reset()
                 env.rollout("random", K, obs_out=obs[0], reward_out=rew[0], done_out=done[0])  # warm
@@ -82,9 +95,10 @@ def main():
                 us = us_launch / max(K, 1)
                 print(json.dumps({"rep": rep, "K": K, "variant": var, "stagger": stg, "lockstep": args.lockstep,
                                   "lib": os.path.basename(_native.LIB_PATH),
+                                  "kernel": _kernel_name(env, K),
                                   "envs": B, "us_per_launch": round(us_launch, 2), "us_per_step": round(us, 2),
                                   "env_steps_per_s": B * K / us_launch * 1e6}), flush=True)
-    L.lbx_set_rollout_variant(0)
+    set_variant(0)
     assert env.status() == 0
 
 
