@@ -10,7 +10,7 @@ HBM instead of sitting in the 256 MB Infinity Cache; terminal observations and e
 are written too.  Env state is resident in HBM before timing.
 
 Two launch shapes run the same steps (bit for bit, tests/test_gpu_api.py):
-  --launch rollout (default): lb_rollout, K = T = 100 vector steps per launch (k_rollout_tpe),
+  --launch rollout (default): lb_rollout, K = T = 100 vector steps per launch (k_rollout_lean),
       the env state in registers between the steps of a launch, every step's outputs in
       its ring slot -- the step-only workload of config 3 (no host policy in the loop);
   --launch step: one lb_step launch per vector step (k_step_tpe), the VecEnv.step() shape
@@ -349,8 +349,8 @@ def main(argv=None):
     if args.launch == "step":
         kname = "k_step_tpe (lb_step, auto-reset inside)" if tpe else "k_step_slice (lb_step)"
     else:
-        kname = ("k_rollout_img (lb_rollout, random policy, auto-reset inside)" if tpe
-                 else "k_rollout_slice (lb_rollout)")
+        # the kernel lb_rollout picks for this launch shape (lb_rollout_kernel, host only)
+        kname = f"{env.rollout_kernel(launches[0])} (lb_rollout, random policy, auto-reset inside)"
     line = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": K,
         "warmup": args.warmup, "ms_per_step": el / K * 1e3, "higher_is_better": True,

@@ -707,8 +707,9 @@ int lb_rollout(void* state, const lb_config* cfg, int64_t num_envs, int32_t poli
         const bool pre = cfg->auto_reset && cfg->episode_length >= steps;
         const int rk = rollout_kernel(cfg, num_envs, steps, obs_out && reward_out && done_out && terminal_obs_out &&
                                                                 ep_stats_out);
-        if (rk == LB_ROLLOUT_LEAN) {  // k_rollout_lean (lbk8s_lean.h)
+        if (rk == LB_ROLLOUT_LEAN) {  // k_rollout_lean (lbk8s_lean.h): LEAN_NB-thread blocks, B % 64 == 0
             const bool e8 = p.E == 8, naive = p.reward_fn == LB_REWARD_NAIVE, act = actions_out != nullptr;
+            const dim3 grid((unsigned)((num_envs + LEAN_NB - 1) / LEAN_NB)), block(LEAN_NB);
 #define LB_LEAN(KIND_, ET_, RT_, NZW_)                                                                           \
             if (naive && act) hipLaunchKernelGGL((k_rollout_lean<KIND_, ET_, RT_, NZW_, true, true>), grid, block, 0, s, p, (int)steps, actions_out); \
             else if (naive) hipLaunchKernelGGL((k_rollout_lean<KIND_, ET_, RT_, NZW_, true, false>), grid, block, 0, s, p, (int)steps, actions_out); \

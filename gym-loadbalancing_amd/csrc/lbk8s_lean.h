@@ -50,18 +50,15 @@ __device__ __forceinline__ uint4 buf_ld_u128(Rsrc r, uint32_t off) {
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
     return make_uint4(v.x, v.y, v.z, v.w);
 }
-#ifndef LB_ST_NOP
-#define LB_ST_NOP "s_nop 1"
-#endif
+// 16-byte stores with every offset in the lane's VGPR and soffset 0.  An SGPR soffset is not
+// safe on gfx950: the compiler's hazard recognizer treats such a store's data registers as free
+// once it has issued (its >64-bit store-data rule excludes that form), and under load an f64
+// VALU write several instructions later still changed the stored data of a quarter of the lanes
+// (lanes 12-15 of every 16; 16 wait states did not help, soffset 0 or a global store did)
 template <int AUX>
-__device__ __forceinline__ void buf_st_f4(float4 v, Rsrc r, uint32_t voff, uint32_t soff) {
+__device__ __forceinline__ void buf_st_f4(float4 v, Rsrc r, uint32_t voff) {
     const u32x4 d{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-    __builtin_amdgcn_raw_buffer_store_b128(d, r, voff, soff, AUX);
-    // the store's data registers stay untouched for 2 wait states after it: with an SGPR
-    // soffset the compiler's hazard recognizer allows the next instruction to overwrite them
-    // (its rule for >64-bit buffer stores excludes that form), and on gfx950 that corrupted
-    // the stored data of a quarter of the lanes under load
-    asm volatile(LB_ST_NOP ::"v"(d.x), "v"(d.y), "v"(d.z), "v"(d.w));
+    __builtin_amdgcn_raw_buffer_store_b128(d, r, voff, 0, AUX);
 }
 
 // draw() with the Philox key laundered through an opaque copy: the 10 rounds' keys are then
@@ -71,7 +68,10 @@ __device__ __forceinline__ U4 draw_o(const Params& p, int64_t env, uint32_t epis
     uint32_t k0 = p.key0, k1 = p.key1;
     asm volatile("" : "+s"(k0), "+s"(k1));
     const uint64_t gid = (uint64_t)(p.env_id_offset + env);
-    return philox((uint32_t)gid, episode, slot, dom | ((uint32_t)(gid >> 32) << 8), k0, k1);
+    // (the counter words too: their loop-invariant parts, hoisted per draw domain, spilled)
+    uint32_t c0 = (uint32_t)gid, hi = (uint32_t)(gid >> 32) << 8;
+    asm volatile("" : "+v"(c0), "+v"(hi));
+    return philox(c0, episode, slot, dom | hi, k0, k1);
 }
 template <int KIND>
 __device__ __forceinline__ int lean_policy(const Params& p, int64_t env, const TEnv& tv, const uint32_t (&em)[TPE_E],
@@ -379,9 +379,30 @@ __device__ __forceinline__ float4 term_piece(const uint32_t* wimg, int el, int p
     return img_piece(A, S, (pc & 1) != 0);
 }
 
+#ifdef LB_TIMELINE  // diagnostic build (tools/timeline_lean.py): per-wave stamps at 6 points of each step
+constexpr int LTL_NP = 6;
+#define LB_LTL(k, i)                                                                                            \
+    do {                                                                                                        \
+        asm volatile("" ::: "memory");                                                                          \
+        if (g_timeline && lane == 0)                                                                            \
+            g_timeline[(env0 / 64) * (2 + K * LTL_NP) + 2 + (k) * LTL_NP + (i)] = __builtin_amdgcn_s_memtime(); \
+        asm volatile("" ::: "memory");                                                                          \
+    } while (0)
+#else
+#define LB_LTL(k, i) ((void)0)
+#endif
+
+// One wave per block: a block's LDS and wave slot are released the moment its wave ends, so
+// the next wave starts there at once (with 4-wave blocks a finished wave's slot waited for its
+// three siblings: 74 % of the wave slots were in use over a 20-step launch)
+#ifndef LB_LEAN_NB
+#define LB_LEAN_NB 64
+#endif
+constexpr int LEAN_NB = LB_LEAN_NB;
+
 template <int KIND, int ET, int RT, int NZW, bool NAIVE, bool ACT>
-__global__ __launch_bounds__(256, 4) void k_rollout_lean(Params p, int K, int32_t* act_out) {
-    constexpr int NB = 256, NW = NB / 64, P = 2 * RT, GT = 64 / P;
+__global__ __launch_bounds__(LEAN_NB, 4) void k_rollout_lean(Params p, int K, int32_t* act_out) {
+    constexpr int NB = LEAN_NB, NW = NB / 64, P = 2 * RT, GT = 64 / P;
     constexpr int FAST = GT < REC_FETCH_MAX ? GT : REC_FETCH_MAX;  // restarts per step of the fast path
     static_assert(ET >= 1 && ET <= TPE_E && (RT == ET || RT == ET + 1), "compile-time geometry");
     __shared__ __attribute__((aligned(16))) uint32_t simg[NW][64 * IMG_W];
@@ -458,6 +479,10 @@ __global__ __launch_bounds__(256, 4) void k_rollout_lean(Params p, int K, int32_
         img_endpoints(me, d, em, v.zcap, olat, ocpu);
     }
 
+    // the state loads have landed (a wait the compiler sees: values it loaded before the
+    // loop and uses on some paths only were otherwise still pending at the loop header,
+    // where its wait for them drained the stores of the previous step)
+    __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0)
     bool new_episode = false;
     uint32_t l0off = (uint32_t)(reinterpret_cast<const char*>(p.lat0) - reinterpret_cast<const char*>(p.lat_lut)) +
                      envi * 8u;
@@ -467,13 +492,16 @@ __global__ __launch_bounds__(256, 4) void k_rollout_lean(Params p, int K, int32_
     // record prefetch of the envs that end at the next step (<= FAST of them: else the slow
     // path in the loop fetches them itself)
     uint4 qn = make_uint4(0u, 0u, 0u, 0u);
+    // (one load in every step, on every lane: lanes without a record to fetch read the wave's
+    // first record chunk, one cache line.  A conditional load merged into qn's register
+    // through a copy, and the compiler drained the whole queue for that copy)
     auto fetch_next = [&](int steps_done) {
         const uint64_t mn = __ballot((int)(steps_done + 1) == p.L);
-        if (mn && __popcll(mn) <= FAST) {
-            int chunk;
-            const int el = rec_fetch_env(mn, lane, chunk);
-            if (el >= 0) qn = buf_ld_u128(blob, rec_off + (uint32_t)(env0 + el) * RO_REC_BYTES + 16u * chunk);
-        }
+        int chunk, ln = lane;
+        asm volatile("" : "+v"(ln));  // (recomputed per step: hoisted, the lane's chunk and slot spilled)
+        const int el = rec_fetch_env(mn, ln, chunk);
+        const uint32_t w0 = rec_off + (uint32_t)env0 * RO_REC_BYTES;
+        qn = buf_ld_u128(blob, el >= 0 ? w0 + (uint32_t)el * RO_REC_BYTES + 16u * chunk : w0);
     };
 
     LPrepL pr;
@@ -540,9 +568,14 @@ __global__ __launch_bounds__(256, 4) void k_rollout_lean(Params p, int K, int32_
         return r;
     };
     pr = prep([](int) {});
+    // (its loads land here, before the loop: pending at the loop header, they made every
+    // wait for the preparation's values inside the loop a vmcnt(0) or close to it)
+    asm volatile("" : "+v"(pr.sel_lat), "+v"(pr.sel_cpu), "+v"(pr.next_lat), "+v"(pr.next_cpu), "+v"(qn.x), "+v"(qn.y),
+                 "+v"(qn.z), "+v"(qn.w));
 
     // one step (k): apply, auto-reset, then step k + 1's preparation with step k's stores
     auto iter = [&](const int k) {
+        LB_LTL(k, 0);
         // issue priority by progress (k_rollout_img): a wave behind the others goes first
         {
             const int pl = 3 - (4 * k) / K;
@@ -551,17 +584,12 @@ __global__ __launch_bounds__(256, 4) void k_rollout_lean(Params p, int K, int32_
             else if (pl == 1) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(0);
         }
-        // every load of the last preparation is consumed here, on every path: its wait is one
-        // counted vmcnt at this point (a value left pending on some path -- a reject never reads
-        // the next latency -- made the compiler drain the whole queue where the register was
-        // next rewritten)
-        asm volatile("" ::"v"(pr.sel_lat), "v"(pr.sel_cpu), "v"(pr.next_lat), "v"(pr.next_cpu), "v"(qn.x), "v"(qn.y),
-                     "v"(qn.z), "v"(qn.w));
         const int a_k = (int)(pr.arz & 0xFFu);
         v.s0 += 1;  // step (<= L: the episode ends there)
         const bool done = (int)(v.s0 & 0xFFFF) == p.L;  // (:472)
         const double reward = lean_apply_l<ET, RT, NAIVE ? (int)LB_REWARD_NAIVE : -1>(p, pr, v, em, ed, me);
         const uint64_t m = __ballot(done);
+        LB_LTL(k, 1);
         if (m) {  // VecEnv auto-reset: episode stats + terminal obs, then the record's episode
             // (the stores below are younger than the prefetched record, so waiting for it does
             // not wait for them; the next gathers do, but a few 16-byte stores issued just
@@ -583,7 +611,7 @@ __global__ __launch_bounds__(256, 4) void k_rollout_lean(Params p, int K, int32_
                 const int tel = term_group_env<P>(grp, lane);
                 if (tel >= 0)
                     buf_st_f4<BUF_NT>(term_piece(wimg, tel, pc), rsrc_of(p.term_obs),
-                                      (uint32_t)((env0 + tel) * P + pc) * 16u, 0);
+                                      (uint32_t)((env0 + tel) * P + pc) * 16u);
                 int chunk;
                 const int rl = rec_fetch_env(grp, lane, chunk);
                 uint4* dst = reinterpret_cast<uint4*>(wimg + rl * IMG_W + 4 * chunk);
@@ -604,33 +632,45 @@ __global__ __launch_bounds__(256, 4) void k_rollout_lean(Params p, int K, int32_
                 pre = false;
             }
         }
+        LB_LTL(k, 2);
         // step k's outputs leave after step k + 1's gathers, spread over its request draws
         const Rsrc out = rsrc_of(p.obs + k * (int64_t)p.B * RT * 8);
         const Rsrc rw = rsrc_of(p.reward + (int64_t)k * p.B), dn = rsrc_of(p.done + (int64_t)k * p.B);
         wave_lds_sync();
+        // copy-out by pieces: store instruction it writes float4s 64 it .. 64 it + 63 of the
+        // wave's obs block (a piece = half a row: lane parity = half), fully coalesced (lanes
+        // storing whole rows, 32 bytes apart, ran 2.3x slower)
         ImgCursor cur = img_cursor(d, lane);
         const bool h = (lane & 1) != 0;
         auto stores = [&](int stage) {
             if (stage == 0) {
+                LB_LTL(k, 3);
                 if (ACT) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)a_k, rsrc_of(act_out + (int64_t)k * p.B),
                                                                envi * 4u, 0, 0);
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)reward), rw, envi * 4u, 0, BUF_NT);
                 __builtin_amdgcn_raw_buffer_store_b8((uint8_t)done, dn, envi, 0, BUF_NT);
             }
             constexpr int per = (P + PREP_STAGES - 1) / PREP_STAGES;
-            // (the scalar offsets from an opaque copy of the wave's base: hoisted out of the
-            // step loop they were 2R SGPRs, spilled and read back with v_readlane per store)
+            // (the wave's base offset from an opaque copy: hoisted out of the step loop, the
+            // per-store offsets were 2R SGPRs, spilled and read back with v_readlane per store)
             uint32_t so = obs_wave + 1024u * (uint32_t)(stage * per);
             asm volatile("" : "+s"(so));
 #pragma unroll
             for (int it = stage * per; it < (stage + 1) * per && it < P; ++it) {
-                buf_st_f4<BUF_NT>(img_read_piece(wimg, cur, h), out, (uint32_t)lane * 16u,
-                                  so + 1024u * (uint32_t)(it - stage * per));
+                buf_st_f4<BUF_NT>(img_read_piece(wimg, cur, h), out,
+                                  (uint32_t)lane * 16u + so + 1024u * (uint32_t)(it - stage * per));
                 img_advance(d, cur);
             }
         };
         if (k + 1 < K) {
             pr = prep(stores);
+            LB_LTL(k, 4);
+            // the loads land here, behind the step's stores (a counted wait), and the values
+            // the next step reads are this statement's, not the loads': none is pending at the
+            // loop header, where a merge of the paths made the compiler's wait a vmcnt(0)
+            asm volatile("" : "+v"(pr.sel_lat), "+v"(pr.sel_cpu), "+v"(pr.next_lat), "+v"(pr.next_cpu), "+v"(qn.x),
+                         "+v"(qn.y), "+v"(qn.z), "+v"(qn.w));
+            LB_LTL(k, 5);
         } else {
             for (int s = 0; s < PREP_STAGES; ++s) stores(s);
         }
@@ -639,10 +679,16 @@ __global__ __launch_bounds__(256, 4) void k_rollout_lean(Params p, int K, int32_
     // (the first step is peeled off the loop: the loop is then entered, like its back edge,
     // with the gathers followed by a step's stores in flight, and the compiler's wait for
     // the gathers is a counted vmcnt instead of the vmcnt(0) the loop entry's shape forced)
+#ifdef LB_TIMELINE
+    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (2 + K * LTL_NP)] = __builtin_amdgcn_s_memrealtime();
+#endif
     if (K > 0) iter(0);
     for (int k = 1; k < K; ++k) iter(k);
     // (the write-back's addresses from an opaque copy of the env index: the compiler would
     // otherwise keep the launch start's 64-bit addresses alive across the loop)
+#ifdef LB_TIMELINE
+    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (2 + K * LTL_NP) + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
     int64_t ew = env;
     asm volatile("" : "+v"(ew));
 #pragma unroll

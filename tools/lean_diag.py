@@ -45,8 +45,9 @@ def run(B, kw, kind="random", K=20, L=20):
                 bi = torch.nonzero(bad_o).cpu().numpy()  # (env, row, col)
                 import collections
                 el = bi[:, 0] % 64
-                piece = el * P + 2 * bi[:, 1] + (bi[:, 2] >= 4)
-                sl, it = piece % 64, piece // 64
+                q = el * R + bi[:, 1]  # row-per-lane copy-out: row q by lane q % 64, round q // 64
+                sl, it = q % 64, q // 64
+                print("   half", collections.Counter((bi[:, 2] >= 4).tolist()))
                 print("   bad cols", collections.Counter(bi[:, 2].tolist()))
                 print("   storing lane", sorted(collections.Counter(sl.tolist()).items())[:40])
                 print("   store instr", sorted(collections.Counter(it.tolist()).items()))
@@ -75,7 +76,7 @@ if __name__ == "__main__":
     if lib:
         from lbk8s import _native
         _native.LIB_PATH = os.path.abspath(lib)
-    run(131072, {})
+    run(65600, {})
     run(131072, {}, K=1, L=20)
     run(131072, dict(reward_function="latency"))
     run(65600, dict(reward_function="multi"))

@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Where a k_rollout_lean step's time goes (diagnostic build with -DLB_TIMELINE:
+exp/liblbk8s_timeline.so).  Each wave's lane 0 stamps s_memtime at 6 points of every step:
+  0 step start | 1 after apply (+ ballot) | 2 after the auto-reset path | 3 stage 0 of the
+  stores (the next step's gathers and record prefetch issued) | 4 every store issued |
+  5 the gathers landed (the counted wait)
+and s_memrealtime (100 MHz) at the launch start / end of the wave, to convert.  Prints the mean
+cycles of each interval over waves and steps (steps 1..K-2), and the wave lifetime.
+
+    python tools/timeline_lean.py --lib exp/liblbk8s_timeline.so --steps 20
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "gym-loadbalancing_amd")]
+NP = 6
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lib", default="exp/liblbk8s_timeline.so")
+    ap.add_argument("--envs", type=int, default=1 << 20)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--lockstep", action="store_true")
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+
+    from lbk8s import LBVecEnv, _native
+    _native.LIB_PATH = os.path.abspath(args.lib)
+    L = _native.lib()
+    L.lbx_set_timeline.argtypes = [C.c_void_p]
+    B, K = args.envs, args.steps
+    env = LBVecEnv(B, seed=0, as_tensors=True)
+    assert env.rollout_kernel(K) == "k_rollout_lean"
+    R, EL = env.cfg.obs_rows, env.cfg.episode_length
+    T = 100
+    obs = torch.empty((T, B, R, 8), dtype=torch.float32, device="cuda")
+    rew = torch.empty((T, B), dtype=torch.float32, device="cuda")
+    done = torch.empty((T, B), dtype=torch.uint8, device="cuda")
+    env.reset()
+    gid = torch.arange(B, device="cuda")
+    for r in range(1, 1 if args.lockstep else EL):
+        env.step_device(None, obs_out=obs[0], reward_out=rew[0], done_out=done[0])
+        env.reset_masked((gid % EL) == r)
+    waves = B // 64
+    tl = torch.zeros((waves, 2 + K * NP), dtype=torch.int64, device="cuda")
+    out = {}
+    for i in range(4):
+        if i == 3:
+            assert L.lbx_set_timeline(tl.data_ptr()) == 0
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        env.rollout("random", K, obs_out=obs[i * K % (T - K + 1)], reward_out=rew[i * K % (T - K + 1)],
+                    done_out=done[i * K % (T - K + 1)])
+        e1.record()
+        torch.cuda.synchronize()
+        out[f"launch{i}_us"] = round(e0.elapsed_time(e1) * 1e3, 1)
+    assert L.lbx_set_timeline(None) == 0
+    a = tl.cpu().numpy()
+    rt0, rt1 = a[:, 0].astype(np.float64), a[:, 1].astype(np.float64)
+    st = a[:, 2:].reshape(waves, K, NP).astype(np.float64)
+    life_rt = (rt1 - rt0) / 100.0  # us
+    life_cy = st[:, K - 1, 4] - st[:, 0, 0]
+    ghz = float(np.median(life_cy[life_rt > 0] / (life_rt[life_rt > 0] * 1e3)))
+    inner = st[:, 1:K - 1, :]
+    nxt = st[:, 2:K, 0]  # next step start
+    d = {"apply": inner[:, :, 1] - inner[:, :, 0], "reset_path": inner[:, :, 2] - inner[:, :, 1],
+         "prep_to_stores": inner[:, :, 3] - inner[:, :, 2], "stores_issue": inner[:, :, 4] - inner[:, :, 3],
+         "wait_gathers": inner[:, :, 5] - inner[:, :, 4], "to_next_step": nxt - inner[:, :, 5]}
+    tot = nxt - inner[:, :, 0]
+    out.update({"clock_ghz_est": round(ghz, 3), "wave_life_us_mean": round(float(life_rt.mean()), 1),
+                "step_cycles_mean": round(float(tot.mean())), "step_us_mean": round(float(tot.mean()) / ghz / 1e3, 2)})
+    out["intervals_cycles_mean"] = {k: round(float(v.mean())) for k, v in d.items()}
+    out["intervals_cycles_p90"] = {k: round(float(np.quantile(v, 0.9))) for k, v in d.items()}
+    first = st[:, 0, :]
+    out["first_step_cycles"] = round(float((st[:, 1, 0] - first[:, 0]).mean()))
+    out["prologue_us_mean"] = round(float(((st[:, 0, 0] - st[:, 0, 0].min()) / ghz / 1e3).mean()), 1)
+    order = np.argsort(rt0)
+    gens = []
+    for g0 in range(0, waves, 4096):
+        idx = order[g0:g0 + 4096]
+        gens.append({"start_us": round(float((rt0[idx].min() - rt0.min()) / 100.0), 1),
+                     "end_us": round(float((rt1[idx].max() - rt0.min()) / 100.0), 1),
+                     "step_cycles": round(float(tot[idx].mean()))})
+    out["generations"] = gens
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
