@@ -526,6 +526,13 @@ int device_cus() {
     return cus;
 }
 
+// k_rollout_lean: one 64-thread block per 64-env group (B % 64 == 0)
+template <int KIND, int ET, int RT, int NZW, bool NAIVE, bool ACT>
+void launch_lean(const Params& p, int64_t B, int steps, int32_t* act, hipStream_t s) {
+    hipLaunchKernelGGL((k_rollout_lean<KIND, ET, RT, NZW, NAIVE, ACT>), dim3((unsigned)((B + LEAN_NB - 1) / LEAN_NB)),
+                       dim3(LEAN_NB), 0, s, p, steps, act);
+}
+
 // Which kernel lb_rollout launches (lb_rollout_kernel reports it, LB_ROLLOUT_*).
 // Per-lane addresses of the thread-per-env rollouts are 32-bit byte offsets from scalar bases
 // (k_rollout_img: the state blob and the ep_stats rows; k_rollout_lean also the obs slot and
@@ -543,7 +550,8 @@ int rollout_kernel(const lb_config* c, int64_t B, int32_t steps, bool outputs_al
     const bool lean_fits = img_fits && (uint64_t)B * R * 32 <= lim;
     const bool lean_shape = (c->num_endpoints == 8 && R == 9 && c->num_nodes <= 32) ||
                             (c->num_endpoints == 6 && R == 7 && c->num_nodes <= 64);
-    if (lean_fits && lean_shape && B % 64 == 0 && B > SMALL_TPE_MAX_B && outputs_all && g_rollout_variant == 0)
+    if (lean_fits && lean_shape && B % 64 == 0 && B > SMALL_TPE_MAX_B && outputs_all &&
+        g_rollout_variant == 0)
         return LB_ROLLOUT_LEAN;
     if (img_fits && g_rollout_variant != 3) return LB_ROLLOUT_IMG;
     return LB_ROLLOUT_TPE;
@@ -709,12 +717,11 @@ int lb_rollout(void* state, const lb_config* cfg, int64_t num_envs, int32_t poli
                                                                 ep_stats_out);
         if (rk == LB_ROLLOUT_LEAN) {  // k_rollout_lean (lbk8s_lean.h): LEAN_NB-thread blocks, B % 64 == 0
             const bool e8 = p.E == 8, naive = p.reward_fn == LB_REWARD_NAIVE, act = actions_out != nullptr;
-            const dim3 grid((unsigned)((num_envs + LEAN_NB - 1) / LEAN_NB)), block(LEAN_NB);
 #define LB_LEAN(KIND_, ET_, RT_, NZW_)                                                                           \
-            if (naive && act) hipLaunchKernelGGL((k_rollout_lean<KIND_, ET_, RT_, NZW_, true, true>), grid, block, 0, s, p, (int)steps, actions_out); \
-            else if (naive) hipLaunchKernelGGL((k_rollout_lean<KIND_, ET_, RT_, NZW_, true, false>), grid, block, 0, s, p, (int)steps, actions_out); \
-            else if (act) hipLaunchKernelGGL((k_rollout_lean<KIND_, ET_, RT_, NZW_, false, true>), grid, block, 0, s, p, (int)steps, actions_out); \
-            else hipLaunchKernelGGL((k_rollout_lean<KIND_, ET_, RT_, NZW_, false, false>), grid, block, 0, s, p, (int)steps, actions_out);
+            if (naive && act) launch_lean<KIND_, ET_, RT_, NZW_, true, true>(p, num_envs, (int)steps, actions_out, s); \
+            else if (naive) launch_lean<KIND_, ET_, RT_, NZW_, true, false>(p, num_envs, (int)steps, actions_out, s); \
+            else if (act) launch_lean<KIND_, ET_, RT_, NZW_, false, true>(p, num_envs, (int)steps, actions_out, s); \
+            else launch_lean<KIND_, ET_, RT_, NZW_, false, false>(p, num_envs, (int)steps, actions_out, s);
 #define LB_LEAN_KIND(KIND_) if (e8) { LB_LEAN(KIND_, 8, 9, 1) } else { LB_LEAN(KIND_, 6, 7, 2) }
             switch (policy) {
             case LB_POLICY_TOPOLOGY_GREEDY: LB_LEAN_KIND(LB_POLICY_TOPOLOGY_GREEDY); break;

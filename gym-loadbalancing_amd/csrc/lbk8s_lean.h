@@ -95,7 +95,8 @@ __device__ __forceinline__ int topo_bf(uint64_t topo, int a, int b) {
 // selected endpoint's 4 table values, and next_request()'s clock already advanced (arrival
 // and dt from the clock the step will see: nothing changes it in between)
 struct LPrepL {
-    uint32_t arz;
+    uint32_t arz;  // a | thr_idx << 8 | rz << 12 | owner(a) << 14 | zone(a) << 17 | type(a) << 19
+    uint32_t jm;   // loads: j(a) | M(owner) + 1 (capped) << 10 | M(a) << 20
     double sel_lat, sel_cpu, next_lat, next_cpu, arr;
     float dt;
 };
@@ -110,11 +111,9 @@ __device__ __forceinline__ double lean_apply_l(const Params& p, const LPrepL& pr
     const bool accept = a < E, reject = a == E;
     const int ai = accept ? a : 0;
     if (!((v.s1 >> S1_RD) & 1)) v.s1 |= 1u << S1_BAD;
-    const uint32_t emA = pick8(em, ai), edA = pick8(ed, ai);
-    const int oA = em_owner(emA);
-    const uint32_t edO = pick8(ed, oA);
-    const int jA = ed_j(edA);
-    const int Mn = ed_M(edO) < CMAX ? ed_M(edO) + 1 : CMAX;
+    // (the selected endpoint's fields as the preparation found them: nothing changed them since)
+    const int oA = (int)((pr.arz >> 14) & 7u);
+    const int jA = (int)(pr.jm & 0x3FFu), Mn = (int)((pr.jm >> 10) & 0x3FFu), MA = (int)(pr.jm >> 20);
     const int jn = jA < CMAX ? jA + 1 : CMAX;
     double reward;
     if (accept) {
@@ -122,15 +121,15 @@ __device__ __forceinline__ double lean_apply_l(const Params& p, const LPrepL& pr
 #pragma unroll
         for (int e = 0; e < TPE_E; ++e)
             if (e < E && e != ai && ed_j(ed[e]) <= jA) ++cnt;
-        const int rz = (int)((v.s1 >> S1_RZ) & 3), zA = em_zone(emA);
+        const int rz = (int)((v.s1 >> S1_RZ) & 3), zA = (int)((pr.arz >> 17) & 3u);
         const int tl = topo_bf(v.topo, rz, zA);
         const uint32_t gnum = (uint32_t)(v.acc2 >> 32) + (uint32_t)(2 * (2 * cnt - (E - 1)));
         v.acc2 = ((uint64_t)gnum << 32) | (uint32_t)((uint32_t)v.acc2 + (uint32_t)tl);
-        v.acc3 += (uint64_t)node_cost(em_type(emA));
+        v.acc3 += (uint64_t)node_cost((int)((pr.arz >> 19) & 7u));
         v.s0 += 1u << 16;                 // acc (<= step <= L <= 1023: no saturation)
         if (rz == zA) v.s1 += 1;          // intra
         xsum_add(v.sum_lat, v.sum_cpu, v.sum_hi, pr.sel_lat, pr.sel_cpu, tl, rz != zA);
-        const uint32_t edA_new = ((oA == ai ? (uint32_t)Mn : (uint32_t)ed_M(edA)) << 20) |
+        const uint32_t edA_new = ((oA == ai ? (uint32_t)Mn : (uint32_t)MA) << 20) |
                                  ((uint32_t)Mn << 10) | (uint32_t)jn;
 #pragma unroll
         for (int e = 0; e < TPE_E; ++e) {  // select-stores over constant indices
@@ -379,6 +378,21 @@ __device__ __forceinline__ float4 term_piece(const uint32_t* wimg, int el, int p
     return img_piece(A, S, (pc & 1) != 0);
 }
 
+// piece 64 it + lane of the wave's obs block from its image: env e = piece / P by a multiply
+// (exact below 64 P pieces), row = (piece - P e) / 2, half = lane parity (P, 64 it even):
+//   row block at 160 e + 16 row = (160 - 8 P) e + 16 (32 it + lane / 2), request block at 160 e + 144
+template <int P>
+__device__ __forceinline__ float4 lean_piece(const uint32_t* wimg, int lane, int it, bool h) {
+    constexpr uint32_t MAG = (65536u + P - 1) / P;
+    static_assert(P % 2 == 0 && 64u * P * (MAG * P - 65536u) < 65536u, "piece / P by multiply, exact below 64 P");
+    const uint32_t e = ((uint32_t)lane * MAG + (uint32_t)it * (64u * MAG)) >> 16;
+    const char* b = reinterpret_cast<const char*>(wimg);
+    const uint4 A = *reinterpret_cast<const uint4*>(b + e * (uint32_t)(IMG_W * 4 - 8 * P) + 16u * (uint32_t)(lane >> 1) +
+                                                    512u * (uint32_t)it);
+    const uint4 S = *reinterpret_cast<const uint4*>(b + e * (uint32_t)(IMG_W * 4) + 4u * IMG_S);
+    return img_piece(A, S, h);
+}
+
 #ifdef LB_TIMELINE  // diagnostic build (tools/timeline_lean.py): per-wave stamps at 6 points of each step
 constexpr int LTL_NP = 6;
 #define LB_LTL(k, i)                                                                                            \
@@ -560,7 +574,9 @@ __global__ __launch_bounds__(LEAN_NB, 4) void k_rollout_lean(Params p, int K, in
         const int rr = (int)bounded(wi.x, 7), n = (int)bounded(wi.y, (uint32_t)p.N);
         const uint64_t word = (NZW > 1 && n >= 32) ? v.nz1 : v.nz0;
         const uint32_t rz = (uint32_t)((word >> (2 * (n & 31))) & 3);
-        r.arz = (uint32_t)a | ((uint32_t)((rr + 6) % 7) << 8) | (rz << 12);
+        r.arz = (uint32_t)a | ((uint32_t)((rr + 6) % 7) << 8) | (rz << 12) | ((uint32_t)oA << 14) |
+                ((uint32_t)em_zone(emA) << 17) | ((uint32_t)em_type(emA) << 19);
+        r.jm = (uint32_t)jA | ((uint32_t)Mn << 10) | ((uint32_t)ed_M(edA) << 20);
         asm volatile("" ::"v"(r.arz) : "memory");
         between(4);
         asm volatile("" ::: "memory");
@@ -640,7 +656,6 @@ __global__ __launch_bounds__(LEAN_NB, 4) void k_rollout_lean(Params p, int K, in
         // copy-out by pieces: store instruction it writes float4s 64 it .. 64 it + 63 of the
         // wave's obs block (a piece = half a row: lane parity = half), fully coalesced (lanes
         // storing whole rows, 32 bytes apart, ran 2.3x slower)
-        ImgCursor cur = img_cursor(d, lane);
         const bool h = (lane & 1) != 0;
         auto stores = [&](int stage) {
             if (stage == 0) {
@@ -655,11 +670,12 @@ __global__ __launch_bounds__(LEAN_NB, 4) void k_rollout_lean(Params p, int K, in
             // per-store offsets were 2R SGPRs, spilled and read back with v_readlane per store)
             uint32_t so = obs_wave + 1024u * (uint32_t)(stage * per);
             asm volatile("" : "+s"(so));
+            int ln = lane;  // (opaque: the pieces' LDS addresses are loop-invariant, and hoisted they spilled)
+            asm volatile("" : "+v"(ln));
 #pragma unroll
             for (int it = stage * per; it < (stage + 1) * per && it < P; ++it) {
-                buf_st_f4<BUF_NT>(img_read_piece(wimg, cur, h), out,
-                                  (uint32_t)lane * 16u + so + 1024u * (uint32_t)(it - stage * per));
-                img_advance(d, cur);
+                buf_st_f4<BUF_NT>(lean_piece<P>(wimg, ln, it, h), out,
+                                  (uint32_t)ln * 16u + so + 1024u * (uint32_t)(it - stage * per));
             }
         };
         if (k + 1 < K) {

@@ -19,4 +19,4 @@ for l in open("gpurun_out/abnb.jsonl"):
     r = json.loads(l); agg[(r["lib"], r["variant"], r.get("kernel"), r["K"])].append(r["us_per_step"])
 for k, v in sorted(agg.items(), key=str): print(k, v, "min", min(v))
 PY
-timeout -k 10 120 python3 tools/timeline_lean.py --steps 20 > gpurun_out/tl20.json && cat gpurun_out/tl20.json
+true
