@@ -247,3 +247,52 @@ def test_replay_sample_gathers_consistent_rows():
                                      o.data_ptr(), no.data_ptr(), a.data_ptr(), r.data_ptr(), d.data_ptr(), None))
     torch.cuda.synchronize()
     assert int((o[:, 0] // 1000).max()) == S - 1
+
+
+def _greedy_vs_uniform(predict, episodes=256, seed=12345):
+    """Mean return of the greedy policy and of the uniform-random policy over the same
+    `episodes` fresh scenarios of run.py's training setup (cli.env_kwargs defaults)."""
+    from lbk8s import LBVecEnv, cli
+    kw = cli.env_kwargs(False, 6, 4, 24, "multi")
+    out = []
+    for policy in (lambda e, o: predict(o).to(torch.int32), lambda e, o: e.policy("random")):
+        env = LBVecEnv(episodes, seed=seed, as_tensors=True, **kw)
+        obs = env.reset()
+        ret = torch.zeros(episodes, dtype=torch.float64, device="cuda")
+        for _ in range(env.cfg.episode_length):
+            obs, r, _, _ = env.step(policy(env, obs))
+            ret += r.to(torch.float64)
+        out.append(float(ret.mean()))
+    return out
+
+
+@pytest.mark.parametrize("device_loop", [True, False])
+def test_dqn_run_py_setup_beats_uniform_random(device_loop):
+    """run.py's DQN setup (8 envs, multi reward, E = 6, learning_starts 10,000) at a tenth of
+    its 200,000 learner steps: the greedy policy beats the uniform-random one on 256 fresh
+    scenarios by a margin of ~10 standard errors (tools/learn_curves.py: +6.7 at 20,000 steps,
+    +7.8 at 200,000; profiles/r04_learn_*.json).  Both loops: the device loop (explore draws
+    on the device, an env without monitor) and the host loop (the CLI's monitored env)."""
+    from lbk8s import LBVecEnv, cli
+    from lbk8s.dqn import DQN_DeepSets
+    if device_loop:
+        env = LBVecEnv(8, seed=0, as_tensors=True, **cli.env_kwargs(False, 6, 4, 24, "multi"))
+    else:
+        env = cli.get_env("loadbalancer", False, 6, 4, 24, "multi", num_envs=8, seed=0, monitor_file=None)
+    model = DQN_DeepSets(env, num_steps=100, n_minibatches=8, seed=1, device_rng=device_loop)
+    model.learn(total_timesteps=20000)
+    greedy, uniform = _greedy_vs_uniform(model.predict)
+    assert greedy > uniform + 3.0, (greedy, uniform)
+
+
+def test_ppo_run_py_setup_beats_uniform_random():
+    """run.py's PPO setup (8 envs x T = 100, 8 minibatches, ent_coef 0.001) for 25 updates
+    (20,000 env steps, a tenth of run.py's): greedy beats uniform random on 256 fresh
+    scenarios (tools/learn_curves.py: +11.2 at 20,000, +17.5 at 200,000)."""
+    from lbk8s import cli
+    from lbk8s.ppo import PPO_DeepSets
+    env = cli.get_env("loadbalancer", False, 6, 4, 24, "multi", num_envs=8, seed=0, monitor_file=None)
+    model = PPO_DeepSets(env, num_steps=100, n_minibatches=8, ent_coef=0.001, seed=2)
+    model.learn(total_timesteps=20000)
+    greedy, uniform = _greedy_vs_uniform(model.predict)
+    assert greedy > uniform + 3.0, (greedy, uniform)
