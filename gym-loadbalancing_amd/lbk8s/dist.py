@@ -30,9 +30,15 @@ def world_info():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def forced_multi():
+    """LBK8S_FORCE_MULTI=1: the multi-rank code path (collectives, split graphs) even in a
+    one-rank process group -- the RCCL path exercised on a one-GPU box."""
+    return os.environ.get("LBK8S_FORCE_MULTI") == "1"
+
+
 def is_multi():
     import torch.distributed as dist
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    return dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1 or forced_multi())
 
 
 def free_port():
@@ -60,7 +66,8 @@ def init_from_env(device_type="cuda", backend=None):
     """Initialise the default process group from the torchrun environment (no-op for one
     process).  GPUs: one per rank (LOCAL_RANK), backend nccl (= RCCL); CPU: gloo.
     LBK8S_DIST_BACKEND=gloo overrides the backend: with it, ranks beyond the visible GPUs
-    share them (LOCAL_RANK mod device count) — a test mode for a one-GPU box.
+    share them (LOCAL_RANK mod device count) — a test mode for a one-GPU box.  With
+    LBK8S_FORCE_MULTI=1 a single process forms a one-rank group (RCCL on a GPU).
     Returns (rank, world, device)."""
     import torch.distributed as dist
     rank, world, local = world_info()
@@ -71,8 +78,12 @@ def init_from_env(device_type="cuda", backend=None):
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or forced_multi()) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:  # (a one-rank group outside torchrun)
+            os.environ.setdefault("MASTER_PORT", str(free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:

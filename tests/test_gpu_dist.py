@@ -54,3 +54,23 @@ def test_cli_nproc_two_ranks(tmp_path):
         assert len(mon.read_text().splitlines()) == 2 + 32 * 2  # header lines + 2 episodes per env
     saved = [p for p in os.listdir(tmp_path) if p.startswith("ppo_deepsets_env_loadbalancer")]
     assert len(saved) == 1
+
+
+def test_rccl_one_rank_multi_path_equals_single_rank(tmp_path):
+    """The RCCL code path on a one-GPU box: one process forms a one-rank nccl (= RCCL)
+    group and runs PPO and DQN with the multi-rank path forced (LBK8S_FORCE_MULTI=1:
+    broadcast, gradient all_reduce between the split HIP graphs, episode-return all_reduce);
+    the result equals the single-rank graph path's bit for bit."""
+    out = tmp_path / "res.json"
+    env = dict(os.environ, LBK8S_DIST_BACKEND="nccl", PYTHONPATH=os.path.join(REPO, "gym-loadbalancing_amd"))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tests", "dist_force_worker.py"), str(out)], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(out.read_text())
+    print(json.dumps(res))
+    assert res["backend"] == "nccl" and res["world"] == 1
+    for algo in ("ppo", "dqn"):
+        assert res[algo]["equal"], res[algo]
+        assert res[algo]["returns_multi"] == res[algo]["returns_single"], res[algo]
