@@ -23,7 +23,8 @@
 // step that ends an episode starts the next one from its record, and the next step's action,
 // table gathers and request draws are issued before the current step's rows are stored.
 // Measured against k_rollout_tpe (tools/roll_variants.py, 2^20 staggered default envs,
-// interleaved, profiles/r03_rollout_variants.jsonl): see DESIGN.md §4.
+// interleaved): see DESIGN.md §4.  At the bench's shapes lb_rollout now runs k_rollout_lean
+// (lbk8s_lean.h); this kernel takes the other thread-per-env launches with L >= K.
 // Tried and dropped (same file): each lane storing its own rows (scattered 16-byte
 // nontemporal stores: 12x slower; plain stores 2x), half the pieces of every env per pass
 // (144-byte runs: 1.7-2.8x slower), 32 envs' whole rows per pass (2 waves per SIMD: equal to

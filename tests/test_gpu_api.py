@@ -270,8 +270,8 @@ def test_vecmonitor_file_during_training(tmp_path):
     (3000, dict(num_endpoints=64, reward_function="multi"), "auto"),
     (40000, dict(num_endpoints=20, reward_function="fairness"), "auto"),       # 4-envs-per-wave slice
     (40000, {}, "slice"),
-    (40000, dict(num_endpoints=6), "tpe"),                                     # k_rollout_tpe, 64-thread blocks
-    (70000, {}, "tpe"),                                                        # k_rollout_tpe, 256-thread blocks
+    (40000, dict(num_endpoints=6), "tpe"),                                     # k_rollout_tpe (L < K), 64-thread blocks
+    (70000, {}, "tpe"),                                                        # k_rollout_tpe (L < K), 256-thread blocks
     (40000, dict(num_nodes=100), "tpe"),                                       # N > 64: K policy + step launches
     (70000, dict(auto_reset=False), "tpe"),      # k_rollout_tpe without auto-reset, envs stepped past L
 ])
@@ -314,11 +314,12 @@ def test_rollout_equals_policy_plus_step(B, kw, geometry, kind):
 @pytest.mark.parametrize("kind", ["random", "endpoint_cpu"])
 @pytest.mark.parametrize("K,L", [(23, 9), (16, 20), (20, 20)])
 def test_rollout_tpe_staggered_equals_policy_plus_step(B, kw, kind, K, L):
-    """k_rollout_tpe with staggered episodes (1/L of the envs finish at every step, the
+    """lb_rollout with staggered episodes (1/L of the envs finish at every step, the
     bench's steady state): == K x (lb_policy + lb_step), bit for bit, including the terminal
-    obs and the episode-stats rows.  L <= K: envs can finish twice in a launch (in-loop
-    block-list resets); L >= K: next episodes drawn into records before the first step
-    (L == K: every env ends exactly once per launch)."""
+    obs and the episode-stats rows.  L < K: k_rollout_tpe (envs can finish twice in a launch:
+    in-loop block-list resets); L >= K: next episodes drawn into records before the first step
+    (L == K: every env ends exactly once per launch) by k_rollout_img, or k_rollout_lean at
+    131,072 default envs -- the kernel lb_rollout_kernel names, asserted below."""
     from lbk8s import LBVecEnv
     envs = [LBVecEnv(B, seed=5, as_tensors=True, episode_length=L, geometry="tpe", **kw) for _ in range(2)]
     gid = torch.arange(B, device="cuda")
@@ -328,6 +329,8 @@ def test_rollout_tpe_staggered_equals_policy_plus_step(B, kw, kind, K, L):
             e.step_device(None)
             e.reset_masked((gid % L) == r)
     a_env, b_env = envs
+    lean = B % 64 == 0 and B > 65536 and kw.get("num_endpoints", 8) in (6, 8)
+    assert a_env.rollout_kernel(K) == ("k_rollout_tpe" if L < K else "k_rollout_lean" if lean else "k_rollout_img")
     R = a_env.cfg.obs_rows
     obs = torch.empty((K, B, R, 8), device="cuda")
     rew = torch.empty((K, B), device="cuda")

@@ -209,9 +209,10 @@ def test_config2_rollout_matches_oracle(oracle_mod):
     (40000, 20, dict(num_endpoints=6, num_nodes=48, num_zones=12, reward_function="multi")),
 ])
 def test_rollout_tpe_staggered_matches_oracle(oracle_mod, B, K, kw):
-    """bench.py's default launch (k_rollout_tpe: K vector steps per launch, the env's random
-    policy, staggered episodes, next episodes drawn into records before the first step since
-    L >= K) against the C oracle stepping one vector step at a time, bit for bit: obs,
+    """lb_rollout with the env's random policy (K vector steps per launch, staggered episodes,
+    next episodes drawn into records before the first step since L >= K: k_rollout_img here,
+    as lb_rollout_kernel reports; k_rollout_lean is tested at its shapes in test_gpu_lean.py)
+    against the C oracle stepping one vector step at a time, bit for bit: obs,
     reward, done, terminal obs, and the state after the launches.  64-thread blocks (40,000
     envs, geometry pinned to tpe) and 256-thread blocks with a partial last block (70,000);
     the default scenario, E = 3 without rejection (fairness reward), config 1's E = 6, N = 48,
@@ -222,6 +223,7 @@ def test_rollout_tpe_staggered_matches_oracle(oracle_mod, B, K, kw):
     L, seed = 20, 99
     cfg = dict(episode_length=L, **kw)
     env = LBVecEnv(B, seed=seed, as_tensors=True, geometry="tpe", **cfg)
+    assert env.rollout_kernel(K) == "k_rollout_img"
     orc = oracle_mod.OracleBatch(cfg, B, trace=False, seed=seed)
     orc.init()
     np.testing.assert_array_equal(env.reset().cpu().numpy(), orc.reset())
