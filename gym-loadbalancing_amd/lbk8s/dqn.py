@@ -438,10 +438,14 @@ class DQN_DeepSets:
                 self.rb.advance_host()
             if train:
                 self._after_train(last)
-            if any(s % 1000 == 0 for s in range(g, last + 1)) or last == total_timesteps - 1:
-                eps = linear_schedule(self.start_e, self.end_e, self.exploration_fraction * total_timesteps, last)
+            marks = [s for s in range(g, last + 1) if s % 1000 == 0 or s == total_timesteps - 1]
+            if marks:
+                # (logged at the 1000-step boundary inside the period, as the host loop logs it;
+                # the returns flushed are those of the whole period)
+                s = marks[0]
+                eps = linear_schedule(self.start_e, self.end_e, self.exploration_fraction * total_timesteps, s)
                 self._flush_returns()
-                self.log_fn(dict(global_step=last, epsilon=eps, sps=(last + 1) / (time.time() - start),
+                self.log_fn(dict(global_step=s, epsilon=eps, sps=(last + 1) / (time.time() - start),
                                  loss=None if loss is None else loss.item(),
                                  ep_return=self.episode_returns[-1] if self.episode_returns else float("nan")))
             g = last + 1
