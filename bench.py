@@ -252,12 +252,14 @@ def main(argv=None):
                 else:
                     i += one_launch(mode, i, end)
 
-        run(0, args.warmup)
         K = args.steps
         # the timed window's launches not covered by whole ring cycles (a window that starts
         # or ends mid-ring, e.g. the driver's --warmup 5 --steps 20: one 20-step launch) are
         # captured as a graph of their own beforehand, so every timed launch is issued by a
-        # graph replay instead of a host-side launch call (the same kernels and arguments)
+        # graph replay instead of a host-side launch call (the same kernels and arguments).
+        # Captured BEFORE the warm-up runs, so the warm-up's launches run right before the
+        # timed window (capturing after them left the GPU idle for the capture: the timed
+        # 20-step launch then ran ~8% slower than the same launch issued back to back)
         seg = None
         if not args.no_graph and (args.warmup % T != 0 or K % T != 0):
             seg = torch.cuda.CUDAGraph()
@@ -268,8 +270,14 @@ def main(argv=None):
                     n = one_launch(mode, i, end, record=False)
                     seg_launches.append(n)
                     i += n
+        run(0, args.warmup)
         del launched[:]
-        ep0 = env.stats()[:, ST_EPISODE].sum().item()
+        # resets in the window: the done flags of the K timed steps when they all still sit in
+        # the ring afterwards (K <= T); otherwise the episode counters before and after.  (An
+        # env.stats() pass right before the window -- 134 MB written at 2^20 envs -- evicted
+        # the env state from the 256 MB Infinity Cache and slowed the timed 20-step launch 7%.)
+        ring_count = K <= T
+        ep0 = None if ring_count else env.stats()[:, ST_EPISODE].sum().item()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         # timed: exactly K steps, barrier + synchronize on both sides; HIP events on the
         # kernels' stream bracket the same launches (their average = the kernel's duration)
@@ -294,7 +302,11 @@ def main(argv=None):
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
         kernel_ms = ev0.elapsed_time(ev1) / K
-        resets = int(env.stats()[:, ST_EPISODE].sum().item() - ep0)
+        if ring_count:
+            slots = [(args.warmup + j) % T for j in range(K)]
+            resets = int(done_ring[slots].to(torch.int64).sum().item())
+        else:
+            resets = int(env.stats()[:, ST_EPISODE].sum().item() - ep0)
         assert env.status() == 0, "kernel flagged bad actions / unreset envs"
         assert kernel_ms <= own_el / K * 1e3 * 1.001, "event window longer than the wall-clock window"
         if world > 1:

@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--lib", default=None, help="another build of liblbk8s.so (an A/B across builds)")
     ap.add_argument("--no-obs", action="store_true", help="launch without the obs output (compute + small outputs)")
     ap.add_argument("--slot0", action="store_true", help="every timed launch writes from ring slot 0")
+    ap.add_argument("--graph", action="store_true", help="issue the timed launches as one captured HIP graph")
+    ap.add_argument("--stats-before", action="store_true",
+                    help="as bench.py: an env.stats() reduction + host sync right before the timed window")
     ap.add_argument("--lockstep", action="store_true",
                     help="no staggering: every env restarts before each measurement (no episode ends "
                          "inside warm-up + timed launches when (launches + 1) * K < L)")
@@ -83,12 +86,26 @@ def main():
                     env.reset()
                 env.rollout("random", K, obs_out=obs[0], reward_out=rew[0], done_out=done[0])  # warm
                 torch.cuda.synchronize()
+                def launches():
+                    for i in range(args.launches):
+                        s = 0 if args.slot0 else (i * K) % max(1, T - K + 1)
+                        env.rollout("random", K, obs_out=None if args.no_obs else obs[s], reward_out=rew[s],
+                                    done_out=done[s])
+                g = None
+                if args.graph:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        launches()
+                    env.rollout("random", K, obs_out=obs[0], reward_out=rew[0], done_out=done[0])  # warm again
+                if args.stats_before:
+                    env.stats()[:, 0].sum().item()
+                torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
-                for i in range(args.launches):
-                    s = 0 if args.slot0 else (i * K) % max(1, T - K + 1)
-                    env.rollout("random", K, obs_out=None if args.no_obs else obs[s], reward_out=rew[s],
-                                done_out=done[s])
+                if g is not None:
+                    g.replay()
+                else:
+                    launches()
                 e1.record(stream)
                 torch.cuda.synchronize()
                 us_launch = e0.elapsed_time(e1) * 1e3 / args.launches
