@@ -314,14 +314,16 @@ __device__ __forceinline__ int rec_fetch_env(uint64_t m, int lane, int& chunk) {
 }
 constexpr int REC_FETCH_MAX = 6;
 
-// the ep_stats row (write_stats_row's values) as 8 paired 16-byte stores
+// the ep_stats row's inputs (write_stats_row's accumulators)
 struct Acc {
     double total;
     uint64_t acc2, acc3, sum_lat, sum_cpu;
     uint32_t sum_hi, s0, s1;
 };
+// the ep_stats row (write_stats_row's values, the LB_ST_* column order) into the lane's LDS
+// image region, 16 doubles = words 0..31
 template <int ET>
-__device__ __forceinline__ void stats_row_store(Rsrc st, uint32_t voff, const Acc& a) {
+__device__ __forceinline__ void stats_row_lds(uint32_t* me, const Acc& a) {
     static_assert(LB_ST_RETURN == 0 && LB_ST_LENGTH == 1 && LB_ST_ACCEPTED == 2 && LB_ST_SUM_LATENCY == 3 &&
                       LB_ST_SUM_TOPOLOGY == 4 && LB_ST_SUM_TOPOLOGY_UPDATED == 5 && LB_ST_SUM_COST == 6 &&
                       LB_ST_SUM_CPU == 7 && LB_ST_INTRA == 8 && LB_ST_INTER == 9 && LB_ST_GINI == 10 &&
@@ -330,12 +332,9 @@ __device__ __forceinline__ void stats_row_store(Rsrc st, uint32_t voff, const Ac
                   "ep_stats column order");
     const Scal s = sc_unpack((uint64_t)a.s0 | ((uint64_t)a.s1 << 32));
     const uint32_t sum_topo = (uint32_t)a.acc2;
-    // one pair per store, computed next to it (all 16 values at once held 17 more registers)
     auto put = [&](int i, double x, double y) {
         const uint64_t lo = (uint64_t)__double_as_longlong(x), hi = (uint64_t)__double_as_longlong(y);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)},
-                                               st, voff + 16u * i, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
+        *reinterpret_cast<uint4*>(me + 4 * i) = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
     };
     double ls, lr, cs, cr;
     put(0, a.total, (double)s.step);
@@ -348,6 +347,21 @@ __device__ __forceinline__ void stats_row_store(Rsrc st, uint32_t voff, const Ac
     put(5, gini_of(a.acc2, s.acc, ET), (double)(uint32_t)(a.acc3 >> 32));
     put(6, lr, cr);
     put(7, (double)((int32_t)a.sum_hi >> XH_D), 0.0);
+}
+// the i-th lowest set bit of m (i < 8), or -1
+__device__ __forceinline__ int nth_env8(uint64_t m, int i) {
+    int el = -1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int b = m ? (int)__builtin_ctzll(m) : -1;
+        if (i == j) el = b;
+        m &= m - 1;
+    }
+    return el;
+}
+__device__ __forceinline__ u32x4 lds_u4(const uint32_t* a) {
+    const uint4 q = *reinterpret_cast<const uint4*>(a);
+    return u32x4{q.x, q.y, q.z, q.w};
 }
 
 // one group of terminal observations: lane l reads piece l % P of env l / P of the group
@@ -610,8 +624,6 @@ __global__ __launch_bounds__(LEAN_NB, 4) void k_rollout_lean(Params p, int K, in
             // (the stores below are younger than the prefetched record, so waiting for it does
             // not wait for them; the next gathers do, but a few 16-byte stores issued just
             // before them cost about nothing next to the gathers' own round trip)
-            if (done) stats_row_store<ET>(rsrc_of(p.ep_stats), envi * (uint32_t)(8 * LB_ST_K),
-                                      Acc{v.total, v.acc2, v.acc3, v.sum_lat, v.sum_cpu, v.sum_hi, v.s0, v.s1});
             wave_lds_sync();  // (apply's image writes, read by other lanes below)
             // groups of up to FAST ending envs: their terminal observations (one store), their
             // records into their image regions (prefetched when the whole step is one group,
@@ -628,17 +640,31 @@ __global__ __launch_bounds__(LEAN_NB, 4) void k_rollout_lean(Params p, int K, in
                 if (tel >= 0)
                     buf_st_f4<BUF_NT>(term_piece(wimg, tel, pc), rsrc_of(p.term_obs),
                                       (uint32_t)((env0 + tel) * P + pc) * 16u);
+                const bool mine = done && ((grp >> lane) & 1);
+                wave_lds_sync();  // (the terminal pieces are read before the rows overwrite them)
+                // the group's episode-statistics rows: each ending env's lane writes its row into
+                // its image region, then ONE store instruction writes them all, 8 lanes (16 bytes
+                // each) per 128-byte row (8 single-lane stores per row ran ~4% slower at K = 20)
+                if (mine)
+                    stats_row_lds<ET>(me, Acc{v.total, v.acc2, v.acc3, v.sum_lat, v.sum_cpu, v.sum_hi, v.s0, v.s1});
+                wave_lds_sync();
+                {
+                    const int sel = nth_env8(grp, lane >> 3), c = lane & 7;
+                    if (sel >= 0)
+                        __builtin_amdgcn_raw_buffer_store_b128(
+                            lds_u4(wimg + sel * IMG_W + 4 * c), rsrc_of(p.ep_stats),
+                            (uint32_t)(env0 + sel) * (uint32_t)(8 * LB_ST_K) + 16u * (uint32_t)c, 0, 0);
+                }
                 int chunk;
                 const int rl = rec_fetch_env(grp, lane, chunk);
                 uint4* dst = reinterpret_cast<uint4*>(wimg + rl * IMG_W + 4 * chunk);
-                wave_lds_sync();  // (the terminal pieces are read before the records overwrite them)
+                wave_lds_sync();  // (the rows are read before the records overwrite them)
                 if (pre) {
                     if (rl >= 0) *dst = qn;
                 } else {
                     if (rl >= 0) *dst = buf_ld_u128(blob, rec_off + (uint32_t)(env0 + rl) * RO_REC_BYTES + 16u * chunk);
                 }
                 wave_lds_sync();
-                const bool mine = done && ((grp >> lane) & 1);
                 lean_restart_group(p, d, wimg, grp, lane, mine, v, em, ed, me);
                 if (mine) {
                     new_episode = true;

@@ -52,7 +52,8 @@ def main():
     if args.lib:
         _native.LIB_PATH = os.path.abspath(args.lib)
     L = _native.lib()
-    if hasattr(L, "lbx_set_rollout_variant"):
+    fn = getattr(L, "lbx_set_rollout_variant", None)
+    if fn is not None and type(fn).__name__ != "_Missing":
         L.lbx_set_rollout_variant.argtypes = [C.c_int]
         set_variant = L.lbx_set_rollout_variant
     else:
