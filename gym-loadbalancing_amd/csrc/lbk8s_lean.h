@@ -12,21 +12,26 @@
 // A step stores ~19 KB per wave (obs block, rewards, done flags).  Every load of the loop is
 // therefore issued BEFORE the stores it would otherwise wait behind:
 //   * step k + 1's 4 table gathers right after its action, step k's obs / reward / done /
-//     action stores after them (spread over step k + 1's request draws);
+//     action stores after them (spread over step k + 1's request draws), and the gathers
+//     waited for at the end of that step (a counted vmcnt behind the step's own stores);
 //   * the record of an env that ends at step k + 1 (the next episode, drawn before the first
 //     step) is fetched in iteration k, next to the gathers: 10 lanes x 16 bytes per env, one
-//     load instruction for up to 6 envs, landing in 4 registers per lane; at its end the wave
-//     drops it into the env's own image region and the env restarts from there, in place;
+//     unconditional load instruction for up to FAST envs, landing in 4 registers per lane; at
+//     its end the wave drops it into the env's own image region and the env restarts from
+//     there, in place;
 //   * the terminal observations leave as one store per group of 64 / 2R envs (lane = piece),
-//     the episode-statistics row as 8 paired 16-byte stores.
+//     the groups' episode-statistics rows as one store per group, staged in LDS.
 // Addresses are scalar buffer descriptors plus 32-bit lane offsets (raw buffer
 // instructions): no 64-bit per-lane address lives in a register, and the compiler cannot
-// strength-reduce the per-step output addresses into per-lane pointers.
-// Compile-time E, R, node-zone words and reward kind keep registers and SGPRs down.
+// strength-reduce the per-step output addresses into per-lane pointers.  Every 16-byte
+// store has soffset 0 (buf_st_f4: an SGPR soffset is unsafe on gfx950, see there).
+// Compile-time E, R, node-zone words and reward kind keep registers and SGPRs down; empty
+// asm statements launder values the compiler would hoist out of the step loop and spill.
 // The record layout is this kernel's own (lean_write_record: scenario words first, the
 // initial latencies last, so the in-place restart never overwrites a word it still needs).
-// Bit for bit K x (lb_policy + lb_step) and the C oracle (tests/test_gpu_api.py,
-// tests/test_gpu_parity.py): the same draws and float64 operations in the same order.
+// Bit for bit K x (lb_policy + lb_step) and the C oracle (tests/test_gpu_lean.py,
+// tests/test_gpu_api.py, tests/test_gpu_parity.py): the same draws and float64 operations
+// in the same order.
 #pragma once
 
 #include "lbk8s_rollout.h"
