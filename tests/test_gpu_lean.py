@@ -133,3 +133,33 @@ def test_lean_not_chosen_outside_its_shapes():
     env = LBVecEnv(131072, seed=1, as_tensors=True)
     assert env.rollout_kernel(20, outputs_all=False) == "k_rollout_img"
     assert env.rollout_kernel(20) == "k_rollout_lean"
+
+
+def test_rollout_past_4gib_takes_64bit_kernel():
+    """Above 4 GiB of state the 32-bit-offset kernels (k_rollout_lean / k_rollout_img) are not
+    used: lb_rollout takes k_rollout_tpe (64-bit indexing), and its launch at such a B
+    equals K x step_device, bit for bit (12,000,000 default envs: a 4.56 GB state blob)."""
+    from lbk8s import LBVecEnv, _native
+    B, K, L = 12_000_000, 3, 3
+    a_env = LBVecEnv(B, seed=9, as_tensors=True, episode_length=L)
+    assert a_env.state.numel() > (1 << 32)
+    assert a_env.rollout_kernel(K) == "k_rollout_tpe"
+    R = a_env.cfg.obs_rows
+    obs = torch.empty((K, B, R, 8), device="cuda")
+    rew = torch.empty((K, B), device="cuda")
+    dn = torch.empty((K, B), dtype=torch.uint8, device="cuda")
+    a_env.reset()
+    a_env.rollout("random", K, obs_out=obs, reward_out=rew, done_out=dn)
+    a_stats, a_term = a_env.stats(), a_env.terminal_obs.clone()
+    del a_env
+    b_env = LBVecEnv(B, seed=9, as_tensors=True, episode_length=L)
+    b_env.reset()
+    for k in range(K):
+        b_env.step_device(None)
+        assert torch.equal(obs[k], b_env.obs), k
+        assert torch.equal(rew[k], b_env.rewards), k
+        assert torch.equal(dn[k], b_env.dones), k
+    assert int(dn[K - 1].sum()) == B
+    assert torch.equal(a_stats, b_env.stats())
+    assert torch.equal(a_term, b_env.terminal_obs)
+    assert b_env.status() == 0
