@@ -163,3 +163,28 @@ def test_rollout_past_4gib_takes_64bit_kernel():
     assert torch.equal(a_stats, b_env.stats())
     assert torch.equal(a_term, b_env.terminal_obs)
     assert b_env.status() == 0
+
+
+def test_lean_shard_equals_slice_of_whole():
+    """A rank's shard (env_id_offset = n) runs the same trajectories as envs n .. 2n - 1 of
+    one 2n-env batch: k_rollout_lean keys every draw (steps and the records of the next
+    episodes) on the global env id, so bench.py --gpus N measures the same work at any N."""
+    from lbk8s import LBVecEnv
+    n, K, L = 131072, 20, 20
+    whole = LBVecEnv(2 * n, seed=3, as_tensors=True, episode_length=L)
+    shard = LBVecEnv(n, seed=3, env_id_offset=n, as_tensors=True, episode_length=L)
+    assert whole.rollout_kernel(K) == "k_rollout_lean" and shard.rollout_kernel(K) == "k_rollout_lean"
+    outs = []
+    for e, B in ((whole, 2 * n), (shard, n)):
+        e.reset()
+        R = e.cfg.obs_rows
+        o = torch.empty((K, B, R, 8), device="cuda")
+        r = torch.empty((K, B), device="cuda")
+        d = torch.empty((K, B), dtype=torch.uint8, device="cuda")
+        for _ in range(2):  # the second launch starts on the episodes the first restarted
+            e.rollout("random", K, obs_out=o, reward_out=r, done_out=d)
+        outs.append((o, r, d, e.stats(), e.terminal_obs))
+    (o1, r1, d1, s1, t1), (o2, r2, d2, s2, t2) = outs
+    assert torch.equal(o1[:, n:], o2) and torch.equal(r1[:, n:], r2) and torch.equal(d1[:, n:], d2)
+    assert torch.equal(s1[n:], s2) and torch.equal(t1[n:], t2)
+    assert int(d2.sum()) == n  # every env ended once per launch (L == K, no stagger)
