@@ -454,15 +454,51 @@ __global__ __launch_bounds__(LEAN_NB, 4) void k_rollout_lean(Params p, int K, in
     const uint32_t rec_off = (uint32_t)(reinterpret_cast<const char*>(p.rec) - reinterpret_cast<const char*>(p.lat_lut));
     const uint32_t cpu0 = (uint32_t)(reinterpret_cast<const char*>(p.cpu_lut) - reinterpret_cast<const char*>(p.lat_lut));
 
+    // the state, issued first: its loads are in flight while the records below are drawn
+    // (the step counter and the episode word first: the record list needs them)
+    LEnv v;
+    uint32_t em[TPE_E], ed[TPE_E];
+    double l0s[TPE_E];
+    {
+        const uint64_t sc = p.sc[env];
+        v.acc3 = p.acc3[env];
+        v.s0 = (uint32_t)sc;
+        v.s1 = (uint32_t)(sc >> 32);
+#pragma unroll
+        for (int e = 0; e < TPE_E; ++e) {
+            em[e] = 0u;
+            ed[e] = 0u;
+            l0s[e] = 0.0;
+            if (e < ET) {
+                const int64_t i = (int64_t)e * p.B + env;
+                l0s[e] = p.lat0[i];
+                em[e] = p.emeta[i];  // (the raw emeta word until the records are drawn)
+                ed[e] = p.edyn[i];
+            }
+        }
+        v.t = p.t[env];
+        v.zcap = p.zcap[env];
+        v.acc2 = p.acc2[env];
+        v.topo = p.topo[env];
+        v.nz0 = p.nzone[env];
+        v.nz1 = NZW > 1 ? p.nzone[p.B + env] : 0;
+        v.sum_lat = p.sum_lat[env];
+        v.sum_cpu = p.sum_cpu[env];
+        v.sum_hi = p.sum_hi[env];
+        v.total = p.total[env];
+        v.last_r = NAIVE ? 0.0 : p.last_r[env];
+        v.dt = 0.f;
+    }
+
     // the next episodes of the envs that end inside the launch, into their records
     {
-        const int to_done = p.L - (int)(p.sc[env] & 0xFFFF);
+        const int to_done = p.L - (int)(v.s0 & 0xFFFF);
         const bool fin = to_done >= 1 && to_done <= K;
         const uint64_t fm = __ballot(fin);
         if (fin) {
             uint32_t* it = wimg + 2 * __popcll(fm & ((1ull << lane) - 1));
             it[0] = (uint32_t)lane;
-            it[1] = (uint32_t)(p.acc3[env] >> 32) + 1;
+            it[1] = (uint32_t)(v.acc3 >> 32) + 1;
         }
         wave_lds_sync();
         const int nf = __popcll(fm), g = lane / RS_W, gl = lane % RS_W;
@@ -473,42 +509,20 @@ __global__ __launch_bounds__(LEAN_NB, 4) void k_rollout_lean(Params p, int K, in
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
 
-    LEnv v;
-    uint32_t em[TPE_E], ed[TPE_E];
+    // the observation image from the state (table reads of the current latency and cpu)
     {
         float olat[TPE_E], ocpu[TPE_E];
 #pragma unroll
         for (int e = 0; e < TPE_E; ++e) {
-            em[e] = 0u;
-            ed[e] = 0u;
             olat[e] = 0.f;
             ocpu[e] = 0.f;
             if (e < ET) {
-                const int64_t i = (int64_t)e * p.B + env;
-                const double l0 = p.lat0[i];
-                const uint32_t m = p.emeta[i];
-                ed[e] = p.edyn[i];
-                em[e] = lem_make(m, l0);
-                olat[e] = (float)lat_of(p, l0, ed[e]);
+                const uint32_t m = em[e];
+                em[e] = lem_make(m, l0s[e]);
+                olat[e] = (float)lat_of(p, l0s[e], ed[e]);
                 ocpu[e] = (float)cpu_of(p, m, ed[e]);
             }
         }
-        v.t = p.t[env];
-        const uint64_t sc = p.sc[env];
-        v.s0 = (uint32_t)sc;
-        v.s1 = (uint32_t)(sc >> 32);
-        v.zcap = p.zcap[env];
-        v.acc2 = p.acc2[env];
-        v.acc3 = p.acc3[env];
-        v.topo = p.topo[env];
-        v.nz0 = p.nzone[env];
-        v.nz1 = NZW > 1 ? p.nzone[p.B + env] : 0;
-        v.sum_lat = p.sum_lat[env];
-        v.sum_cpu = p.sum_cpu[env];
-        v.sum_hi = p.sum_hi[env];
-        v.total = p.total[env];
-        v.last_r = NAIVE ? 0.0 : p.last_r[env];
-        v.dt = 0.f;
         img_endpoints(me, d, em, v.zcap, olat, ocpu);
     }
 
