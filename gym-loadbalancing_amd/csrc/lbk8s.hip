@@ -860,6 +860,9 @@ unsigned ds_grid(int64_t groups) {
     const int64_t want = (groups + DS_BLOCK / 64 - 1) / (DS_BLOCK / 64);
     return (unsigned)std::min<int64_t>(want, device_cus());
 }
+// k_deepsets_fwd numbers its waves wave-major (wave w of block b = w * grid + b): every CU
+// gets a block as soon as there are as many groups as CUs
+unsigned ds_grid_spread(int64_t groups) { return (unsigned)std::min<int64_t>(groups, device_cus()); }
 
 template <int MODE>
 void ds_forward_launch(const DSParams& p, hipStream_t s) {
@@ -868,15 +871,15 @@ void ds_forward_launch(const DSParams& p, hipStream_t s) {
         return;
     }
     // a wave takes P envs per iteration: P = 4 for R <= 16, 2 for R <= 32, else 1 -- fewer
-    // when the batch would leave waves of the chip idle (the DQN vector step's 4096 envs:
-    // 1,024 groups of four filled 128 of the 256 CUs; its 128-set train step)
+    // when the batch would leave SIMDs of the chip idle (the DQN vector step's 4096 envs:
+    // 1,024 groups of four, one per SIMD; its 128-set train step)
     const int ts = (p.R + 15) / 16;
     int P = ts == 1 ? 4 : (ts == 2 ? 2 : 1);
     {
-        const int64_t waves = (int64_t)device_cus() * (DS_BLOCK / 64);
-        while (P > 1 && (p.B + P - 1) / P < waves) P /= 2;
+        const int64_t simds = (int64_t)device_cus() * 4;
+        while (P > 1 && (p.B + P - 1) / P < simds) P /= 2;
     }
-    const unsigned grid = ds_grid((p.B + P - 1) / P);
+    const unsigned grid = ds_grid_spread((p.B + P - 1) / P);
     switch (ts) {
         case 1:
             if (P == 4) hipLaunchKernelGGL((k_deepsets_fwd<1, 4, MODE>), dim3(grid), dim3(DS_BLOCK), 0, s, p);

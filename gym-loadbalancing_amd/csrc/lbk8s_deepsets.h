@@ -323,7 +323,9 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
         *reinterpret_cast<float4*>(W + i) = *reinterpret_cast<const float4*>(p.wfrag + i);
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const int64_t wave = (int64_t)blockIdx.x * (DS_BLOCK / 64) + (threadIdx.x >> 6);
+    // wave-major numbering: a batch of fewer groups than waves puts one wave on each SIMD
+    // of every CU (waves 0-3 of a block sit on its 4 SIMDs) before any SIMD takes a second
+    const int64_t wave = (int64_t)(threadIdx.x >> 6) * gridDim.x + blockIdx.x;
     const int64_t nwaves = (int64_t)gridDim.x * (DS_BLOCK / 64);
     const int R = p.R;
     const int col = lane & 15, grp = lane >> 4;
