@@ -249,32 +249,54 @@ __device__ __forceinline__ void set_max_store(const float (&h)[P * TS][KS], floa
     }
 }
 
-// out = act(Lambda·h - Gamma·max_set(h)), NT 16-row output tiles (4 for 64 outputs)
+// out = act(Lambda·h - Gamma·max_set(h)), NT 16-row output tiles (4 for 64 outputs).
+// Issue order: the four Gamma chains side by side, then per output tile the P*TS set tiles'
+// chains side by side (all four output tiles at once when P*TS <= 2), so consecutive MFMAs
+// are independent (a dependent f32 MFMA waits 40 cycles against 32 for issue, and one chain
+// at a time left the DPP broadcast of each Gamma result on the critical path).  Every
+// element still accumulates Gamma first, then k = 0..KS-1 in order: the same bits.
 template <int TS, int P, int KS, int ACT>
 __device__ __forceinline__ void eq_layer(const float* L, const float* G, const float (&h)[P * TS][KS],
                                          const float (&mb)[KS], float (&out)[P * TS][16], int lane) {
+    constexpr int ST = P * TS;
+    dsf4 g[4];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-        dsf4 g = {0.f, 0.f, 0.f, 0.f};
+    for (int nt = 0; nt < 4; ++nt) g[nt] = dsf4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int k = 0; k < KS; ++k) g = mfma4(G[(nt * KS + k) * 64 + lane], mb[k], g);
+    for (int k = 0; k < KS; ++k)
 #pragma unroll
-        for (int s = 0; s < P; ++s) {
-            dsf4 init;
+        for (int nt = 0; nt < 4; ++nt) g[nt] = mfma4(G[(nt * KS + k) * 64 + lane], mb[k], g[nt]);
+    constexpr int NTB = ST <= 2 ? 4 : 1;  // output tiles per pass
 #pragma unroll
-            for (int i = 0; i < 4; ++i) init[i] = from_col_dyn<P>(g[i], s);
+    for (int nt0 = 0; nt0 < 4; nt0 += NTB) {
+        dsf4 acc[NTB][ST];
 #pragma unroll
-            for (int t = 0; t < TS; ++t) {
-                dsf4 acc = init;
+        for (int j = 0; j < NTB; ++j)
 #pragma unroll
-                for (int k = 0; k < KS; ++k) acc = mfma4(L[(nt * KS + k) * 64 + lane], h[s * TS + t][k], acc);
+            for (int s = 0; s < P; ++s) {
+                dsf4 init;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) init[i] = from_col_dyn<P>(g[nt0 + j][i], s);
+#pragma unroll
+                for (int t = 0; t < TS; ++t) acc[j][s * TS + t] = init;
+            }
+#pragma unroll
+        for (int k = 0; k < KS; ++k)
+#pragma unroll
+            for (int j = 0; j < NTB; ++j) {
+                const float a = L[((nt0 + j) * KS + k) * 64 + lane];
+#pragma unroll
+                for (int st = 0; st < ST; ++st) acc[j][st] = mfma4(a, h[st][k], acc[j][st]);
+            }
+#pragma unroll
+        for (int j = 0; j < NTB; ++j)
+#pragma unroll
+            for (int st = 0; st < ST; ++st)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const float x = acc[i];
-                    out[s * TS + t][4 * nt + i] = ACT == 1 ? act_relu(x) : (ACT == 2 ? act_elu(x) : x);
+                    const float x = acc[j][st][i];
+                    out[st][4 * (nt0 + j) + i] = ACT == 1 ? act_relu(x) : (ACT == 2 ? act_elu(x) : x);
                 }
-            }
-        }
     }
 }
 
@@ -449,16 +471,22 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
                 for (int s = 1; s < P; ++s) r = (col % P == s) ? sm[k * P + s] : r;
                 mc[k] = r * invR;
             }
+            // (the four output tiles' chains side by side; each element: Gamma then Lambda, k in order)
+            dsf4 acc[4];
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt) {
-                dsf4 acc = {0.f, 0.f, 0.f, 0.f};
+            for (int nt = 0; nt < 4; ++nt) acc[nt] = dsf4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int k = 0; k < 16; ++k) acc = mfma4(W[DS_C3G + (nt * 16 + k) * 64 + lane], m2[k], acc);
+            for (int k = 0; k < 16; ++k)
 #pragma unroll
-                for (int k = 0; k < 16; ++k) acc = mfma4(W[DS_C3L + (nt * 16 + k) * 64 + lane], mc[k], acc);
+                for (int nt = 0; nt < 4; ++nt) acc[nt] = mfma4(W[DS_C3G + (nt * 16 + k) * 64 + lane], m2[k], acc[nt]);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) mean[4 * nt + i] = acc[i];
-            }
+            for (int k = 0; k < 16; ++k)
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt) acc[nt] = mfma4(W[DS_C3L + (nt * 16 + k) * 64 + lane], mc[k], acc[nt]);
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) mean[4 * nt + i] = acc[nt][i];
         }
         if (TRAIN) {
             // column c carries env (c mod P): lanes of columns < P store their env's features
@@ -472,15 +500,20 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
             continue;
         }
         float r1[16];
+        {
+            dsf4 acc[4];
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-            dsf4 acc;
+            for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) acc[i] = W[DS_R1B + 16 * nt + 4 * grp + i];
+                for (int i = 0; i < 4; ++i) acc[nt][i] = W[DS_R1B + 16 * nt + 4 * grp + i];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) acc = mfma4(W[DS_R1W + (nt * 16 + k) * 64 + lane], mean[k], acc);
+            for (int k = 0; k < 16; ++k)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) r1[4 * nt + i] = act_elu(acc[i]);
+                for (int nt = 0; nt < 4; ++nt) acc[nt] = mfma4(W[DS_R1W + (nt * 16 + k) * 64 + lane], mean[k], acc[nt]);
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) r1[4 * nt + i] = act_elu(acc[nt][i]);
         }
         dsf4 v = {W[DS_R2B], 0.f, 0.f, 0.f};
 #pragma unroll
