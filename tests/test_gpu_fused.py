@@ -73,6 +73,23 @@ def test_fused_forward_large_batch_and_tail():
         near(value, agent.critic(x), what="value")
 
 
+@pytest.mark.parametrize("R", [9, 20])
+@pytest.mark.parametrize("B", [1, 255, 256, 257, 1023, 1025, 2047, 4095, 4097, 8193])
+def test_fused_forward_batch_sizes_around_the_grid(R, B):
+    """Batch sizes around the launch's choices: P envs per wave (4 / 2 / 1 for R <= 16,
+    fewer when the groups would not cover every SIMD), the grid (one block per CU up to the
+    CU count, waves numbered wave-major), partial last groups."""
+    from lbk8s import fused
+    from lbk8s.deepsets import DeepSetAgent
+    torch.manual_seed(11 * B + R)
+    agent = DeepSetAgent(8).cuda()
+    x = torch.randn(B, R, 8, device="cuda") * 1.5
+    logits, value = fused.deepsets_forward(agent, x, require=True)
+    with torch.no_grad():
+        near(logits, agent.actor(x), what=f"logits B={B} R={R}")
+        near(value, agent.critic(x), what=f"value B={B} R={R}")
+
+
 def test_fused_weights_follow_optimizer_steps():
     from lbk8s import fused
     from lbk8s.deepsets import DeepSetAgent
