@@ -303,6 +303,9 @@ def main(argv=None):
             el = float(t.item())
         kernel_ms = ev0.elapsed_time(ev1) / K
         if ring_count:
+            # (a done flag is a reset only under the VecEnv auto-reset; without it the window's
+            # resets would be the ST_EPISODE count below)
+            assert env.auto_reset, "ring reset count needs auto_reset"
             slots = [(args.warmup + j) % T for j in range(K)]
             resets = int(done_ring[slots].to(torch.int64).sum().item())
         else:

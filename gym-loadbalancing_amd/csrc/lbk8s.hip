@@ -687,6 +687,8 @@ int lb_rollout_kernel(const lb_config* cfg, int64_t num_envs, int32_t steps, int
                       int32_t* kernel_out) {
     if (int r = validate(cfg)) return r;
     if (num_envs < 1 || steps < 0 || !kernel_out) return fail("num_envs < 1, steps < 0 or kernel_out NULL");
+    // (lb_rollout's own preconditions: a launch it would reject has no kernel to name)
+    if (cfg->rng_mode != LB_RNG_PHILOX) return fail("lb_rollout draws in Philox mode only");
     *kernel_out = rollout_kernel(cfg, num_envs, steps, outputs_all != 0);
     return 0;
 }

@@ -481,7 +481,10 @@ __global__ __launch_bounds__(LEAN_NB, 4) void k_rollout_lean(Params p, int K, in
         v.acc2 = p.acc2[env];
         v.topo = p.topo[env];
         v.nz0 = p.nzone[env];
-        v.nz1 = NZW > 1 ? p.nzone[p.B + env] : 0;
+        // (the second node-zone word exists only when the config has more than 32 nodes: the
+        // NZW = 2 instantiation also serves E = 6 configs with N <= 32, whose nzone array
+        // holds one word per env)
+        v.nz1 = NZW > 1 && p.NZW > 1 ? p.nzone[p.B + env] : 0;
         v.sum_lat = p.sum_lat[env];
         v.sum_cpu = p.sum_cpu[env];
         v.sum_hi = p.sum_hi[env];
@@ -767,7 +770,7 @@ __global__ __launch_bounds__(LEAN_NB, 4) void k_rollout_lean(Params p, int K, in
         p.topo[ew] = v.topo;
         p.zcap[ew] = (uint64_t)w[10] | ((uint64_t)w[11] << 32);
         p.nzone[ew] = v.nz0;
-        if (NZW > 1) p.nzone[p.B + ew] = v.nz1;
+        if (NZW > 1 && p.NZW > 1) p.nzone[p.B + ew] = v.nz1;
     }
     p.t[ew] = v.t;
     p.sc[ew] = (uint64_t)v.s0 | ((uint64_t)v.s1 << 32);

@@ -442,12 +442,13 @@ class DQN_DeepSets:
             if marks:
                 # (logged at the 1000-step boundary inside the period, as the host loop logs it;
                 # the returns flushed are those of the whole period)
-                s = marks[0]
-                eps = linear_schedule(self.start_e, self.end_e, self.exploration_fraction * total_timesteps, s)
                 self._flush_returns()
-                self.log_fn(dict(global_step=s, epsilon=eps, sps=(last + 1) / (time.time() - start),
-                                 loss=None if loss is None else loss.item(),
-                                 ep_return=self.episode_returns[-1] if self.episode_returns else float("nan")))
+                now = time.time()
+                for s in marks:  # one line per mark, as the host loop writes them
+                    eps = linear_schedule(self.start_e, self.end_e, self.exploration_fraction * total_timesteps, s)
+                    self.log_fn(dict(global_step=s, epsilon=eps, sps=(s + 1) / (now - start),
+                                     loss=None if loss is None else loss.item(),
+                                     ep_return=self.episode_returns[-1] if self.episode_returns else float("nan")))
             g = last + 1
         return self
 

@@ -49,6 +49,7 @@ def _compare_after(a_env, b_env, B):
     (131072, dict(CFG1, reward_function="multi", latency_weight=1.0, cpu_weight=0.0, gini_weight=0.0)),
     (98304, dict(reward_function="multi", latency_weight=0.4, cpu_weight=0.3, gini_weight=0.3)),
     (98304, dict(num_nodes=28, num_zones=5, reward_function="fairness")),
+    (65536 + 320, dict(num_endpoints=6, reward_function="multi")),  # E = 6, N = 24: one node-zone word
 ])
 @pytest.mark.parametrize("kind", ["random", "topo", "zone_cpu", "endpoint_cpu"])
 @pytest.mark.parametrize("K,L", [(20, 20), (13, 20), (7, 9)])

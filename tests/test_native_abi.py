@@ -156,6 +156,13 @@ def test_rollout_kernel_choice():
     assert _rollout_kernel(1 << 20, 20, auto_reset=False) == "k_rollout_tpe"
     assert _rollout_kernel(1 << 20, 20, num_nodes=100) == "policy+step launches"
     assert _rollout_kernel(4096, 20) == "k_rollout_slice"
+    assert _rollout_kernel(65536 + 320, 20, num_endpoints=6) == "k_rollout_lean"  # E = 6, N = 24: one zone word
+    # lb_rollout's own preconditions hold here too: trace mode has no rollout kernel
+    from lbk8s import LBConfig, _native
+    c = LBConfig().to_c(trace=True)
+    k = C.c_int32(-1)
+    assert _native.lib().lb_rollout_kernel(C.byref(c), 1 << 20, 20, 1, C.byref(k)) != 0
+    assert "Philox" in _native.lib().lb_last_error().decode()
 
 
 def test_rollout_32bit_offsets_guard():
