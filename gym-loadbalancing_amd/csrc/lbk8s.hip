@@ -131,6 +131,7 @@ struct EpLogParams {
     const uint8_t* done;
     const double* ep_stats;
     const float* reward;
+    const double* reward64;
     const int32_t* actions;
     float* ret32;
     float* ep_r32;
@@ -147,7 +148,8 @@ __global__ __launch_bounds__(256) void k_episode_log(EpLogParams p) {
     bool d = false;
     float r32 = 0.f;
     if (live) {
-        r32 = p.ret32[env] + p.reward[env];  // float32, as VecMonitor's episode_returns
+        // VecMonitor's float32 episode_returns += the env's float64 reward: one rounding
+        r32 = p.reward64 ? (float)((double)p.ret32[env] + p.reward64[env]) : p.ret32[env] + p.reward[env];
         d = p.done[env] != 0;
         p.ret32[env] = d ? 0.f : r32;
         if (d && p.ep_r32) p.ep_r32[env] = r32;
@@ -370,7 +372,7 @@ uint64_t align_up(uint64_t x) { return (x + 255) & ~(uint64_t)255; }
 
 struct Offsets {
     uint64_t lat_lut, cpu_lut, lat0, emeta, edyn, t, sc, topo, zcap, nzone, acc2, acc3, sum_lat,
-        sum_cpu, sum_hi, total, last_r, rec, end;
+        sum_cpu, sum_hi, total, last_r, rew64, rec, end;
 };
 
 Offsets offsets(const lb_config* c, int64_t B) {
@@ -396,6 +398,7 @@ Offsets offsets(const lb_config* c, int64_t B) {
     o.sum_hi = take(B * 4);
     o.total = take(B * 8);
     o.last_r = take(B * 8);
+    o.rew64 = take(B * 8);
     // thread-per-env layout: k_rollout_tpe's next-episode records (scratch, per launch)
     o.rec = take(g.tpe ? (uint64_t)B * RO_REC_BYTES : 0);
     o.end = x;
@@ -460,6 +463,7 @@ Params make_params(void* state, const lb_config* c, int64_t B) {
     p.sum_hi = (uint32_t*)(base + o.sum_hi);
     p.total = (double*)(base + o.total);
     p.last_r = (double*)(base + o.last_r);
+    p.rew64 = (double*)(base + o.rew64);
     p.rec = g.tpe ? (uint4*)(base + o.rec) : nullptr;
     p.B = B;
     p.env_id_offset = c->env_id_offset;
@@ -683,6 +687,13 @@ int lb_step(void* state, const lb_config* cfg, int64_t num_envs, const int32_t* 
     return check_launch();
 }
 
+int lb_reward64(void* state, const lb_config* cfg, int64_t num_envs, double** out) {
+    if (int r = validate(cfg)) return r;
+    if (!state || num_envs < 1 || !out) return fail("state/out NULL or num_envs < 1");
+    *out = make_params(state, cfg, num_envs).rew64;
+    return 0;
+}
+
 int lb_rollout_kernel(const lb_config* cfg, int64_t num_envs, int32_t steps, int32_t outputs_all,
                       int32_t* kernel_out) {
     if (int r = validate(cfg)) return r;
@@ -837,11 +848,11 @@ int lb_status(const void* state, const lb_config* cfg, int64_t num_envs, uint32_
 }
 
 int lb_episode_log(int64_t num_envs, const uint8_t* done, const double* ep_stats, const float* reward,
-                   const int32_t* actions, float* ret32, float* ep_r32, int64_t tag, double* log, int64_t cap,
+                   const double* reward64, const int32_t* actions, float* ret32, float* ep_r32, int64_t tag, double* log, int64_t cap,
                    uint32_t* count, void* stream) {
     if (num_envs < 1 || !done || !ep_stats || !reward || !actions || !ret32 || !log || !count || cap < 0)
         return fail("episode log: buffers NULL or num_envs < 1");
-    EpLogParams p{num_envs, done, ep_stats, reward, actions, ret32, ep_r32, tag, log, cap, count};
+    EpLogParams p{num_envs, done, ep_stats, reward, reward64, actions, ret32, ep_r32, tag, log, cap, count};
     hipLaunchKernelGGL(k_episode_log, dim3(env_blocks(num_envs)), dim3(BLOCK), 0, (hipStream_t)stream, p);
     return check_launch();
 }

@@ -185,6 +185,7 @@ struct Params {
     uint32_t* sum_hi;  // [B] their carries and the updated-topology residual D (xsum_add)
     double* total;     // [B]
     double* last_r;    // [B]
+    double* rew64;     // [B] float64 reward of the last lb_step (lb_reward64: VecMonitor's return)
     uint4* rec;        // [B][RO_REC_BYTES / 16] next-episode records (thread-per-env rollout scratch)
     int64_t B, env_id_offset, es, ee;
     int E, Z, N, L, R, EP, NZW, A;

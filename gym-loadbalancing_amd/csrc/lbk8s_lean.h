@@ -46,7 +46,21 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ Rsrc rsrc_of(const void* base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, -1, 0x00020000);
 }
-constexpr int BUF_NT = 2;  // cache-policy bit of a nontemporal access (gfx940+: sc0 = 1, nt = 2)
+constexpr int BUF_NT = 2;
+
+// Occupancy and hoisting guards of the step loop.  At 4 waves per SIMD (128 VGPRs) loop-invariant
+// values the compiler hoists out of the step loop spill, so they are laundered through empty asm
+// and recomputed per step; an experiment build can pick another occupancy and drop the guards.
+#ifndef LB_LEAN_MINW
+#define LB_LEAN_MINW 4
+#endif
+#ifdef LB_LEAN_NOGUARD
+#define LB_GUARD_S(...) ((void)0)
+#define LB_GUARD_V(...) ((void)0)
+#else
+#define LB_GUARD_S(...) asm volatile("" : "+s"(__VA_ARGS__))
+#define LB_GUARD_V(...) asm volatile("" : "+v"(__VA_ARGS__))
+#endif  // cache-policy bit of a nontemporal access (gfx940+: sc0 = 1, nt = 2)
 
 __device__ __forceinline__ double buf_ld_f64(Rsrc r, uint32_t off) {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
@@ -71,11 +85,13 @@ __device__ __forceinline__ void buf_st_f4(float4 v, Rsrc r, uint32_t voff) {
 // loop as 20 SGPRs (which spilled, and were read back with v_readlane in every round)
 __device__ __forceinline__ U4 draw_o(const Params& p, int64_t env, uint32_t episode, uint32_t slot, uint32_t dom) {
     uint32_t k0 = p.key0, k1 = p.key1;
-    asm volatile("" : "+s"(k0), "+s"(k1));
+    LB_GUARD_S(k0);
+    LB_GUARD_S(k1);
     const uint64_t gid = (uint64_t)(p.env_id_offset + env);
     // (the counter words too: their loop-invariant parts, hoisted per draw domain, spilled)
     uint32_t c0 = (uint32_t)gid, hi = (uint32_t)(gid >> 32) << 8;
-    asm volatile("" : "+v"(c0), "+v"(hi));
+    LB_GUARD_V(c0);
+    LB_GUARD_V(hi);
     return philox(c0, episode, slot, dom | hi, k0, k1);
 }
 template <int KIND>
@@ -418,7 +434,7 @@ constexpr int LTL_NP = 6;
     do {                                                                                                        \
         asm volatile("" ::: "memory");                                                                          \
         if (g_timeline && lane == 0)                                                                            \
-            g_timeline[(env0 / 64) * (2 + K * LTL_NP) + 2 + (k) * LTL_NP + (i)] = __builtin_amdgcn_s_memtime(); \
+            g_timeline[(env0 / 64) * (4 + K * LTL_NP) + 4 + (k) * LTL_NP + (i)] = __builtin_amdgcn_s_memtime(); \
         asm volatile("" ::: "memory");                                                                          \
     } while (0)
 #else
@@ -434,7 +450,7 @@ constexpr int LTL_NP = 6;
 constexpr int LEAN_NB = LB_LEAN_NB;
 
 template <int KIND, int ET, int RT, int NZW, bool NAIVE, bool ACT>
-__global__ __launch_bounds__(LEAN_NB, 4) void k_rollout_lean(Params p, int K, int32_t* act_out) {
+__global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p, int K, int32_t* act_out) {
     constexpr int NB = LEAN_NB, NW = NB / 64, P = 2 * RT, GT = 64 / P;
     constexpr int FAST = GT < REC_FETCH_MAX ? GT : REC_FETCH_MAX;  // restarts per step of the fast path
     static_assert(ET >= 1 && ET <= TPE_E && (RT == ET || RT == ET + 1), "compile-time geometry");
@@ -448,6 +464,10 @@ __global__ __launch_bounds__(LEAN_NB, 4) void k_rollout_lean(Params p, int K, in
     // synchronisation below is within the wave)
     const int64_t env0 = (int64_t)blockIdx.x * NB + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63);
     if (env0 >= p.B) return;
+#ifdef LB_TIMELINE
+    if (g_timeline && threadIdx.x % 64 == 0)
+        g_timeline[(env0 / 64) * (4 + K * LTL_NP) + 2] = __builtin_amdgcn_s_memrealtime();
+#endif
     const int64_t env = env0 + lane;
     const uint32_t envi = (uint32_t)env;
     const Rsrc blob = rsrc_of(p.lat_lut);  // tables, lat0 array and records (blob < 4 GiB: host check)
@@ -548,7 +568,7 @@ __global__ __launch_bounds__(LEAN_NB, 4) void k_rollout_lean(Params p, int K, in
     auto fetch_next = [&](int steps_done) {
         const uint64_t mn = __ballot((int)(steps_done + 1) == p.L);
         int chunk, ln = lane;
-        asm volatile("" : "+v"(ln));  // (recomputed per step: hoisted, the lane's chunk and slot spilled)
+        LB_GUARD_V(ln);  // (recomputed per step: hoisted, the lane's chunk and slot spilled)
         const int el = rec_fetch_env(mn, ln, chunk);
         const uint32_t w0 = rec_off + (uint32_t)env0 * RO_REC_BYTES;
         qn = buf_ld_u128(blob, el >= 0 ? w0 + (uint32_t)el * RO_REC_BYTES + 16u * chunk : w0);
@@ -717,9 +737,9 @@ __global__ __launch_bounds__(LEAN_NB, 4) void k_rollout_lean(Params p, int K, in
             // (the wave's base offset from an opaque copy: hoisted out of the step loop, the
             // per-store offsets were 2R SGPRs, spilled and read back with v_readlane per store)
             uint32_t so = obs_wave + 1024u * (uint32_t)(stage * per);
-            asm volatile("" : "+s"(so));
+            LB_GUARD_S(so);
             int ln = lane;  // (opaque: the pieces' LDS addresses are loop-invariant, and hoisted they spilled)
-            asm volatile("" : "+v"(ln));
+            LB_GUARD_V(ln);
 #pragma unroll
             for (int it = stage * per; it < (stage + 1) * per && it < P; ++it) {
                 buf_st_f4<BUF_NT>(lean_piece<P>(wimg, ln, it, h), out,
@@ -744,14 +764,14 @@ __global__ __launch_bounds__(LEAN_NB, 4) void k_rollout_lean(Params p, int K, in
     // with the gathers followed by a step's stores in flight, and the compiler's wait for
     // the gathers is a counted vmcnt instead of the vmcnt(0) the loop entry's shape forced)
 #ifdef LB_TIMELINE
-    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (2 + K * LTL_NP)] = __builtin_amdgcn_s_memrealtime();
+    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (4 + K * LTL_NP)] = __builtin_amdgcn_s_memrealtime();
 #endif
     if (K > 0) iter(0);
     for (int k = 1; k < K; ++k) iter(k);
     // (the write-back's addresses from an opaque copy of the env index: the compiler would
     // otherwise keep the launch start's 64-bit addresses alive across the loop)
 #ifdef LB_TIMELINE
-    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (2 + K * LTL_NP) + 1] = __builtin_amdgcn_s_memrealtime();
+    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (4 + K * LTL_NP) + 1] = __builtin_amdgcn_s_memrealtime();
 #endif
     int64_t ew = env;
     asm volatile("" : "+v"(ew));
@@ -781,6 +801,9 @@ __global__ __launch_bounds__(LEAN_NB, 4) void k_rollout_lean(Params p, int K, in
     p.sum_hi[ew] = v.sum_hi;
     p.total[ew] = v.total;
     if (!NAIVE) p.last_r[ew] = v.last_r;
+#ifdef LB_TIMELINE
+    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (4 + K * LTL_NP) + 3] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 }  // namespace lbk

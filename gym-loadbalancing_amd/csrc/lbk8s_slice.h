@@ -338,7 +338,8 @@ constexpr int RS_W = 8;
 // single-step kernel); a multi-step kernel keeps them in registers and stores them at the end.
 template <int W, int EPL, bool TRACE, bool STORE_ED>
 __device__ __forceinline__ void slice_step_body(const Params& p, int64_t env, int lane, SEnv<EPL>& v, int a,
-                                                float* obs_out, float* reward_out, uint8_t* done_out) {
+                                                float* obs_out, float* reward_out, uint8_t* done_out,
+                                                double* rew64_out) {
     const int E = p.E;
     // ---- phase 1: decode, then every table lookup the step needs, issued together
     v.s.step = v.s.step < 0xFFFF ? v.s.step + 1 : 0xFFFF;
@@ -425,6 +426,7 @@ __device__ __forceinline__ void slice_step_body(const Params& p, int64_t env, in
     const bool done = v.s.step == p.L;
     if (lane == 0) {
         if (reward_out) reward_out[env] = (float)reward;
+        if (rew64_out) rew64_out[env] = reward;
         if (done_out) done_out[env] = (uint8_t)done;
     }
     if (done && p.auto_reset) {
@@ -463,7 +465,7 @@ __global__ __launch_bounds__(BLOCK) void k_step_slice(Params p) {
     SEnv<EPL> v;
     slice_load<W, EPL>(p, env, lane, v);
     const int a = p.actions ? p.actions[env] : random_action(p, env, v.acc3, v.s.step);  // fused random policy
-    slice_step_body<W, EPL, TRACE, true>(p, env, lane, v, a, p.obs, p.reward, p.done);
+    slice_step_body<W, EPL, TRACE, true>(p, env, lane, v, a, p.obs, p.reward, p.done, p.rew64);
     if (lane == 0) slice_store_scalars<EPL>(p, env, v);
 }
 
@@ -516,7 +518,7 @@ __global__ __launch_bounds__(BLOCK) void k_rollout_slice(Params p, int kind, int
         if (act_out && lane == 0) act_out[k * p.B + env] = a;
         slice_step_body<W, EPL, false, false>(p, env, lane, v, a, p.obs ? p.obs + k * obs_slot : nullptr,
                                                p.reward ? p.reward + k * p.B : nullptr,
-                                               p.done ? p.done + k * p.B : nullptr);
+                                               p.done ? p.done + k * p.B : nullptr, nullptr);
     }
 #pragma unroll
     for (int k = 0; k < EPL; ++k) {

@@ -576,6 +576,7 @@ __global__ __launch_bounds__(NB) void k_step_tpe(Params p) {
                                                                 nullptr);
     if (live) {
         if (p.reward) *(p.reward + env) = ((float)reward);
+        if (p.rew64) p.rew64[env] = reward;
         if (p.done) p.done[env] = (uint8_t)done;
     }
 

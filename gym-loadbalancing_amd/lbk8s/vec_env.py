@@ -176,6 +176,11 @@ class LBVecEnv:
         self._t_start = time.time()
         self._host_cache = {}
         self._monitor = _MonitorWriter(monitor_file, self._t_start, self.info_keywords) if monitor_file else None
+        # the float64 rewards of the last lb_step, inside the state blob (lb_reward64): VecMonitor
+        # adds them to its float32 returns with one rounding (lb_episode_log)
+        ptr = C.c_void_p()
+        _native.check(self._L.lb_reward64(self._ptr(self.state), C.byref(self._c), B, C.byref(ptr)))
+        self._rew64 = ptr
         if self.monitor:  # VecMonitor: float32 running returns and the device episode log
             self._ret32 = torch.zeros(B, dtype=torch.float32, device=dev)
             self._ep_r32 = torch.zeros(B, dtype=torch.float32, device=dev)
@@ -388,7 +393,7 @@ class LBVecEnv:
         r = self.rewards if rewards is None else rewards
         a = self.actions if actions is None else actions
         _native.check(self._L.lb_episode_log(
-            self.num_envs, self._ptr(d), self._ptr(self.ep_stats), self._ptr(r), self._ptr(a),
+            self.num_envs, self._ptr(d), self._ptr(self.ep_stats), self._ptr(r), self._rew64, self._ptr(a),
             self._ptr(self._ret32), self._ptr(self._ep_r32), len(self._log_times), self._ptr(self._log),
             self.num_envs, self._ptr(self._log_count), self._stream()))
         self._log_times.append(time.time())

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LBK8S_ABI_VERSION 8
+#define LBK8S_ABI_VERSION 9
 
 /* reward_function names of loadbalancer_k8s_env.py:20-31 */
 enum { LB_REWARD_NAIVE = 0, LB_REWARD_LATENCY = 1, LB_REWARD_FAIRNESS = 2, LB_REWARD_MULTI = 3 };
@@ -313,18 +313,28 @@ int lb_replay_sample(int64_t num_envs, int32_t obs_floats, int64_t slots, int32_
                      float* next_obs_out, int64_t* actions_out, float* rewards_out, float* dones_out, void* stream);
 
 /* ---- Episode log (SB3 VecMonitor, run.py:122) -------------------------------------------
- * After a vector step: every env's float32 running return ret32[b] += reward[b] (VecMonitor
- * sums the float32 rewards, stable_baselines3 vec_monitor.py), and every env with done[b]
+ * After a vector step: every env's float32 running return ret32[b] += reward, and every env
+ * with done[b]
  * appends one LB_EPLOG_W-double row to log [cap][LB_EPLOG_W] at an index taken from the
  * device counter *count (rows past cap are dropped; *count still counts them), then its
  * ret32 restarts at 0 (ep_r32[b] keeps the finished return; may be NULL).  Row: the env's
  * ep_stats row (LB_ST_K doubles), then the float32 return, the step's reward, its action,
  * the env index and `tag` (the caller's step counter; rows are unordered within a call).
- * Only the finished envs' rows move: the log grows with episodes, not with num_envs. */
+ * Only the finished envs' rows move: the log grows with episodes, not with num_envs.
+ * The return: VecMonitor's episode_returns is a float32 array and the SubprocVecEnv rewards it
+ * adds are float64 (the env's Python floats, run.py:114-122), so numpy rounds the sum ONCE:
+ * ret32 = float32(float64(ret32) + r64).  With reward64 (the env's lb_reward64 array: the
+ * float64 rewards of its last lb_step) the kernel does exactly that; with reward64 NULL it adds
+ * the float32 reward (a second rounding, for callers without the float64 values). */
 #define LB_EPLOG_W 24
+/* The float64 reward of every env's last lb_step (get_reward() :516-567, the Python float the
+ * reference's step() returns at :513) lives in the state blob; *out receives its device address
+ * (num_envs doubles).  Host only: pointer arithmetic on the layout of (cfg, num_envs).
+ * lb_step writes it (every kernel behind lb_step); lb_rollout does not. */
+int lb_reward64(void* state, const lb_config* cfg, int64_t num_envs, double** out);
 enum { LB_EPLOG_RET32 = 16, LB_EPLOG_REWARD = 17, LB_EPLOG_ACTION = 18, LB_EPLOG_ENV = 19, LB_EPLOG_TAG = 20 };
 int lb_episode_log(int64_t num_envs, const uint8_t* done, const double* ep_stats, const float* reward,
-                   const int32_t* actions, float* ret32, float* ep_r32, int64_t tag, double* log, int64_t cap,
+                   const double* reward64, const int32_t* actions, float* ret32, float* ep_r32, int64_t tag, double* log, int64_t cap,
                    uint32_t* count, void* stream);
 
 /* ---- Fused deep-sets training -----------------------------

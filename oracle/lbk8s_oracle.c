@@ -76,6 +76,7 @@ typedef struct {
     double *topo;     /* [B*Z*Z] */
     /* per-env scalars [B] */
     double *t, *dt, *sel_lat, *sel_topo, *sel_cpu, *total_reward;
+    double *last_rw;  /* the float64 reward of the last step (get_reward() :516-567) */
     unsigned __int128 *sum_lat, *sum_topo_upd, *sum_cpu;  /* exact sums of the lists, x 2^52 */
     int64_t *sum_topo, *sum_cost;
     int32_t *step, *acc, *intra, *inter, *penalty, *pending, *req_zone, *req_thr, *req_node;
@@ -177,7 +178,7 @@ void* orc_create(const orc_cfg* cfg, int64_t B) {
     ALLOC(s->node_type, BN); ALLOC(s->node_zone, BN); ALLOC(s->node_cpu, BN);
     ALLOC(s->zone_cap, B * s->Z); ALLOC(s->topo, B * s->Z * s->Z);
     ALLOC(s->t, B); ALLOC(s->dt, B); ALLOC(s->sel_lat, B); ALLOC(s->sel_topo, B); ALLOC(s->sel_cpu, B);
-    ALLOC(s->total_reward, B); ALLOC(s->sum_lat, B); ALLOC(s->sum_topo_upd, B); ALLOC(s->sum_cpu, B);
+    ALLOC(s->total_reward, B); ALLOC(s->last_rw, B); ALLOC(s->sum_lat, B); ALLOC(s->sum_topo_upd, B); ALLOC(s->sum_cpu, B);
     ALLOC(s->sum_topo, B); ALLOC(s->sum_cost, B);
     ALLOC(s->step, B); ALLOC(s->acc, B); ALLOC(s->intra, B); ALLOC(s->inter, B); ALLOC(s->penalty, B);
     ALLOC(s->pending, B); ALLOC(s->req_zone, B); ALLOC(s->req_thr, B); ALLOC(s->req_node, B);
@@ -190,7 +191,7 @@ void orc_destroy(void* h) {
     orc_env* s = h;
     void* ptrs[] = {s->ep_node, s->ep_zone, s->ep_cap, s->ep_cpu, s->ep_lat, s->ep_topo, s->loads,
                     s->node_type, s->node_zone, s->node_cpu, s->zone_cap, s->topo, s->t, s->dt,
-                    s->sel_lat, s->sel_topo, s->sel_cpu, s->total_reward, s->sum_lat,
+                    s->sel_lat, s->sel_topo, s->sel_cpu, s->total_reward, s->last_rw, s->sum_lat,
                     s->sum_topo_upd, s->sum_cpu, s->sum_topo, s->sum_cost, s->step, s->acc,
                     s->intra, s->inter, s->penalty, s->pending, s->req_zone, s->req_thr,
                     s->req_node, s->episode, s->was_reset};
@@ -463,6 +464,7 @@ void orc_step(void* h, const int32_t* actions, float* obs, float* reward, uint8_
         } /* else: unrecognised action, penalty stale (:685-686) */
         double rw = reward_of(s, b);
         s->total_reward[b] += rw;
+        s->last_rw[b] = rw;
         double x1, x2;
         int r, n;
         if (st_tr) { x1 = st_tr->x1[b]; x2 = st_tr->x2[b]; r = st_tr->r[b]; n = st_tr->n[b]; }
@@ -485,6 +487,13 @@ void orc_step(void* h, const int32_t* actions, float* obs, float* reward, uint8_
         }
         if (obs) write_obs(s, b, obs);
     }
+}
+
+/* the float64 rewards of the last orc_step (what the reference's step() returns, :513, before
+ * SubprocVecEnv / VecMonitor see it: run.py:114-122) */
+void orc_last_reward64(void* h, double* out) {
+    orc_env* s = h;
+    for (int64_t b = 0; b < s->B; ++b) out[b] = s->last_rw[b];
 }
 
 void orc_get_stats(void* h, double* out) {

@@ -59,6 +59,7 @@ def lib():
         L.orc_step.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                C.c_void_p, C.c_void_p, C.POINTER(_StepTrace), C.POINTER(_ResetTrace)]
         L.orc_get_stats.argtypes = [C.c_void_p, C.c_void_p]
+        L.orc_last_reward64.argtypes = [C.c_void_p, C.c_void_p]
         L.orc_policy_greedy.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
         L.orc_policy_random.argtypes = [C.c_void_p, C.c_void_p]
         L.orc_get_field.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
@@ -154,6 +155,12 @@ class OracleBatch:
         st = np.zeros((self.B, ST_K), np.float64)
         lib().orc_get_stats(self.h, _p(st))
         return st
+
+    def last_reward64(self):
+        """(B,) float64: each env's reward of the last step() before the float32 cast."""
+        out = np.zeros(self.B, np.float64)
+        lib().orc_last_reward64(self.h, _p(out))
+        return out
 
     def field(self, name):
         n = {"t": 1, "step": 1, "req_zone": 1, "req_thr": 1, "dt": 1}.get(name)

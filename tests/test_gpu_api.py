@@ -389,3 +389,40 @@ def test_run_baselines_greedy_matches_oracle(oracle_mod, tmp_path):
                 got = rows[i]
                 for k in CSV_FIELDS[:-1]:  # (execution_time is wall clock)
                     assert float(got[k]) == float(exp[k]), (fname, i, k)
+
+
+@pytest.mark.parametrize("B,E", [(512, 8), (300, 64)])  # thread-per-env and slice step kernels
+def test_vecmonitor_return_rounds_once(oracle_mod, B, E):
+    """SB3 VecMonitor (run.py:114-122) keeps float32 episode_returns and adds the float64
+    rewards SubprocVecEnv hands it (the env's Python floats), so numpy rounds each sum once:
+    ret32 = float32(float64(ret32) + r64).  The monitor's `r` (infos[i]["episode"]["r"]) is
+    checked against that restatement driven by the C oracle's float64 rewards, on a
+    multi-reward scenario where rounding twice (float32(ret32 + float32(r64))) differs."""
+    from lbk8s import LBVecEnv
+    L = 25
+    cfg = dict(num_endpoints=E, episode_length=L, reward_function="multi")
+    env = LBVecEnv(B, seed=31, monitor=True, **cfg)
+    orc = oracle_mod.OracleBatch(cfg, B, trace=False, seed=31)
+    orc.init()
+    np.testing.assert_array_equal(env.reset(), orc.reset())
+    ret = np.zeros(B, np.float32)   # VecMonitor.episode_returns
+    ret2 = np.zeros(B, np.float32)  # the same sums rounded twice
+    rng = np.random.default_rng(5)
+    episodes = differ = 0
+    for s in range(3 * L):
+        a = rng.integers(0, E + 1, size=B).astype(np.int32)
+        _, r, d, infos = env.step(a)
+        _, r2, d2, _, _ = orc.step(a)
+        r64 = orc.last_reward64()
+        np.testing.assert_array_equal(r, r2)
+        np.testing.assert_array_equal(r, r64.astype(np.float32))
+        ret += r64  # numpy: float32 array += float64 array -> computed in float64, cast once
+        ret2 += r64.astype(np.float32)
+        for i in np.flatnonzero(d):
+            assert infos[i]["episode"]["r"] == float(ret[i]), (s, i)
+            episodes += 1
+            differ += int(ret[i] != ret2[i])
+        ret[d] = 0
+        ret2[d] = 0
+    assert episodes == 3 * B
+    assert differ > 0  # the scenario does tell one rounding from two

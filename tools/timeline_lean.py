@@ -48,7 +48,7 @@ def main():
         env.step_device(None, obs_out=obs[0], reward_out=rew[0], done_out=done[0])
         env.reset_masked((gid % EL) == r)
     waves = B // 64
-    tl = torch.zeros((waves, 2 + K * NP), dtype=torch.int64, device="cuda")
+    tl = torch.zeros((waves, 4 + K * NP), dtype=torch.int64, device="cuda")
     out = {}
     for i in range(4):
         if i == 3:
@@ -63,9 +63,10 @@ def main():
     assert L.lbx_set_timeline(None) == 0
     a = tl.cpu().numpy()
     rt0, rt1 = a[:, 0].astype(np.float64), a[:, 1].astype(np.float64)
-    st = a[:, 2:].reshape(waves, K, NP).astype(np.float64)
+    st = a[:, 4:].reshape(waves, K, NP).astype(np.float64)
+    ent, ext = a[:, 2].astype(np.float64), a[:, 3].astype(np.float64)
     life_rt = (rt1 - rt0) / 100.0  # us
-    life_cy = st[:, K - 1, 4] - st[:, 0, 0]
+    life_cy = st[:, K - 1, 2] - st[:, 0, 0]  # (stamp 4 is not taken in the last step)
     ghz = float(np.median(life_cy[life_rt > 0] / (life_rt[life_rt > 0] * 1e3)))
     inner = st[:, 1:K - 1, :]
     nxt = st[:, 2:K, 0]  # next step start
@@ -79,13 +80,21 @@ def main():
     out["intervals_cycles_p90"] = {k: round(float(np.quantile(v, 0.9))) for k, v in d.items()}
     first = st[:, 0, :]
     out["first_step_cycles"] = round(float((st[:, 1, 0] - first[:, 0]).mean()))
-    out["prologue_us_mean"] = round(float(((st[:, 0, 0] - st[:, 0, 0].min()) / ghz / 1e3).mean()), 1)
-    order = np.argsort(rt0)
+    # realtime stamps (100 MHz): kernel entry, loop start, loop end, exit (write-back issued)
+    t00 = ent.min()
+    q = lambda x: [round(float(np.quantile(x, f)), 1) for f in (0.1, 0.5, 0.9, 1.0)]
+    out["prologue_us_q10_50_90_max"] = q((rt0 - ent) / 100.0)
+    out["epilogue_us_q10_50_90_max"] = q((ext - rt1) / 100.0)
+    out["loop_us_q10_50_90_max"] = q((rt1 - rt0) / 100.0)
+    out["entry_after_first_us_q10_50_90_max"] = q((ent - t00) / 100.0)
+    out["exit_before_last_us_q10_50_90_max"] = q((ext.max() - ext) / 100.0)
+    out["span_us"] = round(float((ext.max() - t00) / 100.0), 1)
+    order = np.argsort(ent)
     gens = []
     for g0 in range(0, waves, 4096):
         idx = order[g0:g0 + 4096]
-        gens.append({"start_us": round(float((rt0[idx].min() - rt0.min()) / 100.0), 1),
-                     "end_us": round(float((rt1[idx].max() - rt0.min()) / 100.0), 1),
+        gens.append({"start_us": round(float((ent[idx].min() - t00) / 100.0), 1),
+                     "end_us": round(float((ext[idx].max() - t00) / 100.0), 1),
                      "step_cycles": round(float(tot[idx].mean()))})
     out["generations"] = gens
     print(json.dumps(out))
