@@ -429,12 +429,12 @@ __device__ __forceinline__ float4 lean_piece(const uint32_t* wimg, int lane, int
 }
 
 #ifdef LB_TIMELINE  // diagnostic build (tools/timeline_lean.py): per-wave stamps at 6 points of each step
-constexpr int LTL_NP = 6;
+constexpr int LTL_NP = 6, LTL_H = 8;  // per wave: 8 header words, then 6 stamps per step
 #define LB_LTL(k, i)                                                                                            \
     do {                                                                                                        \
         asm volatile("" ::: "memory");                                                                          \
         if (g_timeline && lane == 0)                                                                            \
-            g_timeline[(env0 / 64) * (4 + K * LTL_NP) + 4 + (k) * LTL_NP + (i)] = __builtin_amdgcn_s_memtime(); \
+            g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP) + LTL_H + (k) * LTL_NP + (i)] = __builtin_amdgcn_s_memtime(); \
         asm volatile("" ::: "memory");                                                                          \
     } while (0)
 #else
@@ -466,7 +466,11 @@ __global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p
     if (env0 >= p.B) return;
 #ifdef LB_TIMELINE
     if (g_timeline && threadIdx.x % 64 == 0)
-        g_timeline[(env0 / 64) * (4 + K * LTL_NP) + 2] = __builtin_amdgcn_s_memrealtime();
+        g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP) + 2] = __builtin_amdgcn_s_memrealtime();
+    if (g_timeline && threadIdx.x % 64 == 0) {  // where the wave runs: HW_ID (cu, simd, se, ...), XCC_ID
+        g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP) + 6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP) + 7] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    }
 #endif
     const int64_t env = env0 + lane;
     const uint32_t envi = (uint32_t)env;
@@ -531,6 +535,9 @@ __global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p
         }
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
+#ifdef LB_TIMELINE
+    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP) + 4] = __builtin_amdgcn_s_memrealtime();
+#endif
 
     // the observation image from the state (table reads of the current latency and cpu)
     {
@@ -553,6 +560,9 @@ __global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p
     // loop and uses on some paths only were otherwise still pending at the loop header,
     // where its wait for them drained the stores of the previous step)
     __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0)
+#ifdef LB_TIMELINE
+    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP) + 5] = __builtin_amdgcn_s_memrealtime();
+#endif
     bool new_episode = false;
     uint32_t l0off = (uint32_t)(reinterpret_cast<const char*>(p.lat0) - reinterpret_cast<const char*>(p.lat_lut)) +
                      envi * 8u;
@@ -764,14 +774,14 @@ __global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p
     // with the gathers followed by a step's stores in flight, and the compiler's wait for
     // the gathers is a counted vmcnt instead of the vmcnt(0) the loop entry's shape forced)
 #ifdef LB_TIMELINE
-    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (4 + K * LTL_NP)] = __builtin_amdgcn_s_memrealtime();
+    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP)] = __builtin_amdgcn_s_memrealtime();
 #endif
     if (K > 0) iter(0);
     for (int k = 1; k < K; ++k) iter(k);
     // (the write-back's addresses from an opaque copy of the env index: the compiler would
     // otherwise keep the launch start's 64-bit addresses alive across the loop)
 #ifdef LB_TIMELINE
-    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (4 + K * LTL_NP) + 1] = __builtin_amdgcn_s_memrealtime();
+    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP) + 1] = __builtin_amdgcn_s_memrealtime();
 #endif
     int64_t ew = env;
     asm volatile("" : "+v"(ew));
@@ -802,7 +812,7 @@ __global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p
     p.total[ew] = v.total;
     if (!NAIVE) p.last_r[ew] = v.last_r;
 #ifdef LB_TIMELINE
-    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (4 + K * LTL_NP) + 3] = __builtin_amdgcn_s_memrealtime();
+    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP) + 3] = __builtin_amdgcn_s_memrealtime();
 #endif
 }
 

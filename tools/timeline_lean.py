@@ -18,6 +18,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "gym-loadbalancing_amd")]
 NP = 6
+NH = 8  # header: loop start, loop end, entry, exit, records drawn, image built (realtime), HW_ID, XCC_ID
 
 
 def main():
@@ -26,6 +27,7 @@ def main():
     ap.add_argument("--envs", type=int, default=1 << 20)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--lockstep", action="store_true")
+    ap.add_argument("--save", default=None, help="write the raw per-wave stamps (npz) here")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -48,7 +50,7 @@ def main():
         env.step_device(None, obs_out=obs[0], reward_out=rew[0], done_out=done[0])
         env.reset_masked((gid % EL) == r)
     waves = B // 64
-    tl = torch.zeros((waves, 4 + K * NP), dtype=torch.int64, device="cuda")
+    tl = torch.zeros((waves, NH + K * NP), dtype=torch.int64, device="cuda")
     out = {}
     for i in range(4):
         if i == 3:
@@ -63,7 +65,7 @@ def main():
     assert L.lbx_set_timeline(None) == 0
     a = tl.cpu().numpy()
     rt0, rt1 = a[:, 0].astype(np.float64), a[:, 1].astype(np.float64)
-    st = a[:, 4:].reshape(waves, K, NP).astype(np.float64)
+    st = a[:, NH:].reshape(waves, K, NP).astype(np.float64)
     ent, ext = a[:, 2].astype(np.float64), a[:, 3].astype(np.float64)
     life_rt = (rt1 - rt0) / 100.0  # us
     life_cy = st[:, K - 1, 2] - st[:, 0, 0]  # (stamp 4 is not taken in the last step)
@@ -83,12 +85,33 @@ def main():
     # realtime stamps (100 MHz): kernel entry, loop start, loop end, exit (write-back issued)
     t00 = ent.min()
     q = lambda x: [round(float(np.quantile(x, f)), 1) for f in (0.1, 0.5, 0.9, 1.0)]
+    rec, img = a[:, 4].astype(np.float64), a[:, 5].astype(np.float64)
     out["prologue_us_q10_50_90_max"] = q((rt0 - ent) / 100.0)
+    out["pro_records_us_q10_50_90_max"] = q((rec - ent) / 100.0)
+    out["pro_image_us_q10_50_90_max"] = q((img - rec) / 100.0)
+    out["pro_first_prep_us_q10_50_90_max"] = q((rt0 - img) / 100.0)
     out["epilogue_us_q10_50_90_max"] = q((ext - rt1) / 100.0)
     out["loop_us_q10_50_90_max"] = q((rt1 - rt0) / 100.0)
     out["entry_after_first_us_q10_50_90_max"] = q((ent - t00) / 100.0)
     out["exit_before_last_us_q10_50_90_max"] = q((ext.max() - ext) / 100.0)
     out["span_us"] = round(float((ext.max() - t00) / 100.0), 1)
+    # where the slow waves run: wave life (entry -> exit) by XCC, by SIMD, by shader engine
+    hw, xcc = a[:, 6].astype(np.int64), a[:, 7].astype(np.int64) & 0xF
+    life = (ext - ent) / 100.0
+    simd, cu, se = (hw >> 4) & 3, (hw >> 8) & 15, (hw >> 13) & 7
+    by = lambda key, n: {int(i): [int((key == i).sum()), round(float(life[key == i].mean()), 1)] for i in range(n)
+                         if (key == i).any()}
+    out["life_by_xcc"] = by(xcc, 16)
+    out["life_by_simd"] = by(simd, 4)
+    out["life_by_se"] = by(se, 8)
+    out["life_by_cu"] = by(cu, 16)
+    cid = xcc * 1024 + se * 64 + cu * 4 + simd
+    u, inv, cnt = np.unique(cid, return_inverse=True, return_counts=True)
+    out["waves_per_simd_hist"] = {int(k): int(v) for k, v in zip(*np.unique(cnt, return_counts=True))}
+    # per SIMD: its waves' mean life; spread of that over SIMDs, and within-SIMD spread
+    ms = np.array([life[inv == i].mean() for i in range(len(u))])
+    out["simd_mean_life_q10_50_90"] = [round(float(np.quantile(ms, f)), 1) for f in (0.1, 0.5, 0.9)]
+    out["life_q10_50_90_max"] = q(life)
     order = np.argsort(ent)
     gens = []
     for g0 in range(0, waves, 4096):
@@ -97,6 +120,8 @@ def main():
                      "end_us": round(float((ext[idx].max() - t00) / 100.0), 1),
                      "step_cycles": round(float(tot[idx].mean()))})
     out["generations"] = gens
+    if args.save:
+        np.savez_compressed(args.save, stamps=a)
     print(json.dumps(out))
 
 
