@@ -867,6 +867,9 @@ int lb_ds_pack(const lb_ds_weights* w, float* frag_out, void* stream) {
 
 }  // extern "C"
 
+#ifndef LB_DS_WAVES_PER_SIMD
+#define LB_DS_WAVES_PER_SIMD 1
+#endif
 namespace {
 // persistent grid for the deep-sets kernels (the weight image is staged once per block)
 unsigned ds_grid(int64_t groups) {
@@ -889,7 +892,7 @@ void ds_forward_launch(const DSParams& p, hipStream_t s) {
     const int ts = (p.R + 15) / 16;
     int P = ts == 1 ? 4 : (ts == 2 ? 2 : 1);
     {
-        const int64_t simds = (int64_t)device_cus() * 4;
+        const int64_t simds = (int64_t)device_cus() * 4 * LB_DS_WAVES_PER_SIMD;
         while (P > 1 && (p.B + P - 1) / P < simds) P /= 2;
     }
     const unsigned grid = ds_grid_spread((p.B + P - 1) / P);

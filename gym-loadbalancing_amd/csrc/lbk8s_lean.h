@@ -182,18 +182,43 @@ __device__ __forceinline__ double lean_apply_l(const Params& p, const LPrepL& pr
 //   words 0..7 emeta (em_pack) | 8,9 topo | 10,11 zcap | 12,13 nz0 | 14,15 nz1 | 16,17 x1 |
 //   18,19 x2 | 20 thr_idx | rz << 8 | 21..23 - | 24..39 lat0 (f64) of endpoints 0..7
 constexpr uint32_t LREC_LAT0 = 96;  // byte offset of lat0[0]
+// after the restart (which reads the record into the image region), words 12..23 hold the ended
+// episode's accumulators until the launch's end: total, acc2 | sum_lat, sum_cpu | cost (acc3's
+// low word), sum_hi, s0, s1
+constexpr uint32_t LREC_ACC = 12;
+__device__ __forceinline__ float4 u4f(double a, uint64_t b) {
+    const uint64_t x = (uint64_t)__double_as_longlong(a);
+    return make_float4(__uint_as_float((uint32_t)x), __uint_as_float((uint32_t)(x >> 32)), __uint_as_float((uint32_t)b),
+                       __uint_as_float((uint32_t)(b >> 32)));
+}
+__device__ __forceinline__ float4 u4f(uint64_t a, uint64_t b) {
+    return make_float4(__uint_as_float((uint32_t)a), __uint_as_float((uint32_t)(a >> 32)), __uint_as_float((uint32_t)b),
+                       __uint_as_float((uint32_t)(b >> 32)));
+}
 
-// reset()'s draws for one env (the same map and owner rule as tpe_write_record), W lanes
+// reset()'s draws for one env (the same map and owner rule as tpe_write_record), 8 lanes.
+// Each Philox block is drawn once per env: lane l draws nodes l, l + 8, ... (the first three
+// of them, nodes < 24, packed and handed to the endpoint lanes whose host they are, instead of
+// a second draw of the host node per endpoint), endpoint l, and ONE of the episode's four
+// remaining blocks by its role: lanes 0 / 1 the request's X block (x1 / x2: one log each),
+// lane 2 its I block, lanes 3 / 4 the topology blocks (8 Philox blocks per lane before: 5).
 template <int W>
 __device__ __forceinline__ void lean_write_record(const Params& p, int64_t env, uint32_t episode, int lane) {
+    static_assert(W == 8, "eight lanes per record (the node packing covers nodes < 24 = 3 x 8)");
     uint64_t zc = 0, nz0 = 0, nz1 = 0;
+    uint32_t hp01 = 0, hp2 = 0;  // this lane's nodes lane, lane + 8 (16 bits each), lane + 16: ty | zo << 3 | cpu << 5
     for (int w = 0; w < p.NZW; ++w) {  // nodes (:349-373)
         uint64_t word = 0;
-        for (int n = 32 * w + lane; n < 32 * (w + 1) && n < p.N; n += W) {
+        int j = 0;
+        for (int n = 32 * w + lane; n < 32 * (w + 1) && n < p.N; n += W, ++j) {
             int ty, zo, cpu;
             node_draw<false>(p, env, episode, n, ty, zo, cpu);
             zc += (uint64_t)node_cpu_int(ty) << (16 * zo);
             word |= (uint64_t)zo << (2 * (n & 31));
+            const uint32_t hp = (uint32_t)ty | ((uint32_t)zo << 3) | ((uint32_t)cpu << 5);
+            if (w == 0 && j == 0) hp01 |= hp;
+            if (w == 0 && j == 1) hp01 |= hp << 16;
+            if (w == 0 && j == 2) hp2 = hp;
         }
         word = slice_or64<W>(word);
         if (w == 0) nz0 = word;
@@ -212,25 +237,35 @@ __device__ __forceinline__ void lean_write_record(const Params& p, int64_t env, 
         const int nd2 = (int)shfl_u32<W>((uint32_t)node, e2);
         if (nd2 == node && e2 < owner) owner = e2;
     }
+    // the host node's draws, from the lane that drew it (node n: lane n % 8, its (n / 8)-th draw)
+    const uint32_t ha = shfl_u32<W>(hp01, node & 7), hb = shfl_u32<W>(hp2, node & 7);
+    const uint32_t hp = (node >> 3) == 0 ? (ha & 0xFFFFu) : (node >> 3) == 1 ? (ha >> 16) : hb;
     uint32_t* out = reinterpret_cast<uint32_t*>(p.rec + env * (RO_REC_BYTES / 16));
     if (lane < p.E) {
-        int ty, zo, cpu;
-        node_draw<false>(p, env, episode, node, ty, zo, cpu);
+        const int ty = (int)(hp & 7u), zo = (int)((hp >> 3) & 3u), cpu = (int)((hp >> 5) & 0x7Fu);
         const uint64_t lb = (uint64_t)__double_as_longlong(lat0);
         *reinterpret_cast<uint2*>(out + 24 + 2 * lane) = make_uint2((uint32_t)lb, (uint32_t)(lb >> 32));
         out[lane] = em_pack(zo, owner, ty, cpu, node);
     }
-    const uint64_t topo = scen_topo(p, env, episode);  // (:331-338)
-    double x1, x2;  // next_request() closing reset() (:397)
-    int r, n;
-    slice_request_draws<W, false>(p, env, episode, 0, lane, true, x1, x2, r, n);
+    // the topology (:331-338) and next_request() closing reset() (:397): one block per lane
+    const int role = lane;
+    const U4 w = draw(p, env, episode, role == 4 ? 1u : 0u,
+                      role == 2 ? D_REQ_I : (role == 3 || role == 4) ? D_TOPO : D_REQ_X);
+    const double e = role == 1 ? std_exp(w.z, w.w) : std_exp(w.x, w.y);
+    const double x1 = p.inv_rate * shfl_f64<W>(e, 0), x2 = p.call * shfl_f64<W>(e, 1);
+    const int r = (int)bounded(shfl_u32<W>(w.x, 2), 7), n = (int)bounded(shfl_u32<W>(w.y, 2), (uint32_t)p.N);
+    const uint32_t a0 = shfl_u32<W>(w.x, 3), a1 = shfl_u32<W>(w.y, 3), a2 = shfl_u32<W>(w.z, 3),
+                   a3 = shfl_u32<W>(w.w, 3), b0 = shfl_u32<W>(w.x, 4), b1 = shfl_u32<W>(w.y, 4);
     if (lane == 0) {
+        const uint64_t topo = (uint64_t)(1 + bounded(a0, 499)) | ((uint64_t)(1 + bounded(a1, 499)) << 9) |
+                              ((uint64_t)(1 + bounded(a2, 499)) << 18) | ((uint64_t)(1 + bounded(a3, 499)) << 27) |
+                              ((uint64_t)(1 + bounded(b0, 499)) << 36) | ((uint64_t)(1 + bounded(b1, 499)) << 45);
         const int rz = (int)(((n < 32 ? nz0 : nz1) >> (2 * (n & 31))) & 3);
-        const uint64_t w[6] = {topo, zc, nz0, nz1, (uint64_t)__double_as_longlong(x1),
-                               (uint64_t)__double_as_longlong(x2)};
+        const uint64_t wd[6] = {topo, zc, nz0, nz1, (uint64_t)__double_as_longlong(x1),
+                                (uint64_t)__double_as_longlong(x2)};
 #pragma unroll
         for (int j = 0; j < 6; ++j)
-            *reinterpret_cast<uint2*>(out + 8 + 2 * j) = make_uint2((uint32_t)w[j], (uint32_t)(w[j] >> 32));
+            *reinterpret_cast<uint2*>(out + 8 + 2 * j) = make_uint2((uint32_t)wd[j], (uint32_t)(wd[j] >> 32));
         out[20] = (uint32_t)((r + 6) % 7) | ((uint32_t)rz << 8);
     }
 }
@@ -693,20 +728,6 @@ __global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p
                     buf_st_f4<BUF_NT>(term_piece(wimg, tel, pc), rsrc_of(p.term_obs),
                                       (uint32_t)((env0 + tel) * P + pc) * 16u);
                 const bool mine = done && ((grp >> lane) & 1);
-                wave_lds_sync();  // (the terminal pieces are read before the rows overwrite them)
-                // the group's episode-statistics rows: each ending env's lane writes its row into
-                // its image region, then ONE store instruction writes them all, 8 lanes (16 bytes
-                // each) per 128-byte row (8 single-lane stores per row ran ~4% slower at K = 20)
-                if (mine)
-                    stats_row_lds<ET>(me, Acc{v.total, v.acc2, v.acc3, v.sum_lat, v.sum_cpu, v.sum_hi, v.s0, v.s1});
-                wave_lds_sync();
-                {
-                    const int sel = nth_env8(grp, lane >> 3), c = lane & 7;
-                    if (sel >= 0)
-                        __builtin_amdgcn_raw_buffer_store_b128(
-                            lds_u4(wimg + sel * IMG_W + 4 * c), rsrc_of(p.ep_stats),
-                            (uint32_t)(env0 + sel) * (uint32_t)(8 * LB_ST_K) + 16u * (uint32_t)c, 0, 0);
-                }
                 int chunk;
                 const int rl = rec_fetch_env(grp, lane, chunk);
                 uint4* dst = reinterpret_cast<uint4*>(wimg + rl * IMG_W + 4 * chunk);
@@ -715,6 +736,17 @@ __global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p
                     if (rl >= 0) *dst = qn;
                 } else {
                     if (rl >= 0) *dst = buf_ld_u128(blob, rec_off + (uint32_t)(env0 + rl) * RO_REC_BYTES + 16u * chunk);
+                }
+                // the ended episode's accumulators, for its episode-statistics row at the launch's
+                // end (an env ends at most once in a launch: L >= K), into words 12..23 of its
+                // record, which only the restart reads (they are in the image region now)
+                if (mine) {
+                    const uint32_t o = rec_off + envi * RO_REC_BYTES + 4u * LREC_ACC;
+                    buf_st_f4<0>(u4f(v.total, v.acc2), blob, o);
+                    buf_st_f4<0>(u4f(v.sum_lat, v.sum_cpu), blob, o + 16u);
+                    buf_st_f4<0>(make_float4(__uint_as_float((uint32_t)v.acc3), __uint_as_float(v.sum_hi),
+                                             __uint_as_float(v.s0), __uint_as_float(v.s1)),
+                                 blob, o + 32u);
                 }
                 wave_lds_sync();
                 lean_restart_group(p, d, wimg, grp, lane, mine, v, em, ed, me);
@@ -783,6 +815,32 @@ __global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p
 #ifdef LB_TIMELINE
     if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP) + 1] = __builtin_amdgcn_s_memrealtime();
 #endif
+    // the episode-statistics rows of the envs that ended in the launch (write_stats_row's values),
+    // from the accumulators their lanes saved at the restart: one pass for the wave, each lane
+    // its row into its image region (the image is not read again), then 8 lanes (16 bytes each)
+    // per 128-byte row, one store instruction per 8 envs
+    {
+        const uint64_t endm = __ballot(new_episode);
+        if (endm) {
+            if (new_episode) {
+                const uint32_t o = rec_off + envi * RO_REC_BYTES + 4u * LREC_ACC;
+                const uint4 q0 = buf_ld_u128(blob, o), q1 = buf_ld_u128(blob, o + 16u), q2 = buf_ld_u128(blob, o + 32u);
+                auto u64 = [](uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); };
+                const uint64_t acc3 = ((uint64_t)((uint32_t)(v.acc3 >> 32) - 1u) << 32) | q2.x;  // (the ended episode)
+                stats_row_lds<ET>(me, Acc{__longlong_as_double((long long)u64(q0.x, q0.y)), u64(q0.z, q0.w), acc3,
+                                          u64(q1.x, q1.y), u64(q1.z, q1.w), q2.y, q2.z, q2.w});
+            }
+            wave_lds_sync();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int el = 8 * i + (lane >> 3), c = lane & 7;
+                if ((endm >> el) & 1)
+                    __builtin_amdgcn_raw_buffer_store_b128(lds_u4(wimg + el * IMG_W + 4 * c), rsrc_of(p.ep_stats),
+                                                           (uint32_t)(env0 + el) * (uint32_t)(8 * LB_ST_K) + 16u * (uint32_t)c,
+                                                           0, 0);
+            }
+        }
+    }
     int64_t ew = env;
     asm volatile("" : "+v"(ew));
 #pragma unroll

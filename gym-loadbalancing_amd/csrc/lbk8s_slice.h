@@ -332,41 +332,50 @@ __global__ __launch_bounds__(BLOCK) void k_reset_slice(Params p) {
 // lanes per env of the thread-per-env step's auto-reset (k_step_tpe, lbk8s_tpe.h)
 constexpr int RS_W = 8;
 
-// One step() (:403-513) of the slice's env held in registers, fused with next_request(),
-// get_state(), reward, done and auto-reset: action a in, obs / reward / done of this step
-// out (NULL = skip).  STORE_ED: write the changed history counters back at once (the
-// single-step kernel); a multi-step kernel keeps them in registers and stores them at the end.
-template <int W, int EPL, bool TRACE, bool STORE_ED>
-__device__ __forceinline__ void slice_step_body(const Params& p, int64_t env, int lane, SEnv<EPL>& v, int a,
-                                                float* obs_out, float* reward_out, uint8_t* done_out,
-                                                double* rew64_out) {
+// One step() (:403-513) of the slice's env held in registers, in three parts:
+//   slice_prep   the action decoded and the selected endpoint's 4 table values gathered
+//                (issued, not waited for);
+//   slice_apply  take_action, reward, next_request(), done and the VecEnv auto-reset
+//                (terminal obs, episode stats, reset()), on the registers;
+//   slice_obs    get_state() of the step's result.
+// The single-step kernel runs them in order; the rollout issues step k + 1's gathers before
+// step k's obs / reward / done stores, which they would otherwise wait behind (s_waitcnt
+// vmcnt retires a wave's memory operations in issue order, stores included).
+struct SPrep {
+    int a, ai, oA, jA, Mn, jn;
+    uint32_t emA;
+    double lat0A, lut_selA, sel_cpu, next_lat, next_cpu;
+};
+template <int W, int EPL>
+__device__ __forceinline__ SPrep slice_prep(const Params& p, const SEnv<EPL>& v, int a) {
     const int E = p.E;
-    // ---- phase 1: decode, then every table lookup the step needs, issued together
-    v.s.step = v.s.step < 0xFFFF ? v.s.step + 1 : 0xFFFF;
+    SPrep r;
+    r.a = a;
     const bool accept = a >= -E && a < E;
-    const bool reject = a == E;
-    if (a < -E) v.s.bad = 1;  // reference: IndexError; here: treated as unrecognised
-    if (!v.s.reset_done) v.s.bad = 1;
-    const int ai = accept ? (a < 0 ? a + E : a) : 0;
-    const int src = ai % W, sk = ai / W;
-    const uint32_t emA = shfl_u32<W>(sel<EPL>(v.em, sk), src);
+    r.ai = accept ? (a < 0 ? a + E : a) : 0;
+    const int src = r.ai % W, sk = r.ai / W;
+    r.emA = shfl_u32<W>(sel<EPL>(v.em, sk), src);
     const uint32_t edA = shfl_u32<W>(sel<EPL>(v.ed, sk), src);
-    const double lat0A = shfl_f64<W>(sel<EPL>(v.lat0, sk), src);
-    const int oA = em_owner(emA);
-    const uint32_t edO = shfl_u32<W>(sel<EPL>(v.ed, oA / W), oA % W);
-    const int jA = ed_j(edA);
-    const int Mn = ed_M(edO) < CMAX ? ed_M(edO) + 1 : CMAX;
-    const int jn = jA < CMAX ? jA + 1 : CMAX;
-    const int k0A = (int)lat0A, c0A = em_c0(emA);
+    r.lat0A = shfl_f64<W>(sel<EPL>(v.lat0, sk), src);
+    r.oA = em_owner(r.emA);
+    const uint32_t edO = shfl_u32<W>(sel<EPL>(v.ed, r.oA / W), r.oA % W);
+    r.jA = ed_j(edA);
+    r.Mn = ed_M(edO) < CMAX ? ed_M(edO) + 1 : CMAX;
+    r.jn = r.jA < CMAX ? r.jA + 1 : CMAX;
+    const int k0A = (int)r.lat0A, c0A = em_c0(r.emA);
     // selected endpoint before (selected_*) and after (inc+dec) this step's update
-    const double lut_selA = p.lat_lut[(jA) * LAT_ROWS + k0A];
-    const double sel_cpu = p.cpu_lut[(ed_m(edA)) * CPU_ROWS + c0A];
-    const double next_lat = p.lat_lut[(jn) * LAT_ROWS + k0A];
-    const double next_cpu = p.cpu_lut[(Mn) * CPU_ROWS + c0A];
+    r.lut_selA = p.lat_lut[(r.jA) * LAT_ROWS + k0A];
+    r.sel_cpu = p.cpu_lut[(ed_m(edA)) * CPU_ROWS + c0A];
+    r.next_lat = p.lat_lut[(r.jn) * LAT_ROWS + k0A];
+    r.next_cpu = p.cpu_lut[(r.Mn) * CPU_ROWS + c0A];
+    return r;
+}
+// the observed values of every endpoint from the history counters (table rows 0 are the
+// initial values: only endpoints selected this episode (j > 0) / refreshed (m > 0) gather)
+template <int EPL>
+__device__ __forceinline__ void slice_observe(const Params& p, SEnv<EPL>& v) {
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) {  // observed values of every endpoint
-        // table rows 0 are the initial values: only endpoints selected this episode
-        // (j > 0) / refreshed (m > 0) gather from the LUTs
+    for (int k = 0; k < EPL; ++k) {
         const int j = ed_j(v.ed[k]), m = ed_m(v.ed[k]);
         double l = v.lat0[k], c = (double)em_c0(v.em[k]);
         if (j) l = p.lat_lut[j * LAT_ROWS + (int)v.lat0[k]];
@@ -374,12 +383,23 @@ __device__ __forceinline__ void slice_step_body(const Params& p, int64_t env, in
         v.olat[k] = (float)l;
         v.ocpu[k] = (float)c;
     }
-
-    // ---- take_action (:578-686)
+}
+// take_action (:578-686), reward, next_request (:1131-1163), done (:472) and the auto-reset;
+// returns the reward, done in `done`.  STORE_ED: write the changed history counters back at
+// once (the single-step kernel; a multi-step kernel keeps them in registers).
+template <int W, int EPL, bool TRACE, bool STORE_ED>
+__device__ __forceinline__ double slice_apply(const Params& p, int64_t env, int lane, SEnv<EPL>& v, const SPrep& pr,
+                                              bool& done) {
+    const int E = p.E, a = pr.a, ai = pr.ai, oA = pr.oA, jA = pr.jA, Mn = pr.Mn, jn = pr.jn;
+    v.s.step = v.s.step < 0xFFFF ? v.s.step + 1 : 0xFFFF;
+    const bool accept = a >= -E && a < E;
+    const bool reject = a == E;
+    if (a < -E) v.s.bad = 1;  // reference: IndexError; here: treated as unrecognised
+    if (!v.s.reset_done) v.s.bad = 1;
     double reward;
     if (accept) {
-        const int zA = em_zone(emA);
-        const double sel_lat = jA == 0 ? lat0A : lut_selA;
+        const int zA = em_zone(pr.emA);
+        const double sel_lat = jA == 0 ? pr.lat0A : pr.lut_selA;
         const int tl = topo_val(v.topo, v.s.rz, zA);
         // O(E) Gini numerator update for avg_load_served[ai] += 1 (:631)
         int cnt = 0;
@@ -392,10 +412,10 @@ __device__ __forceinline__ void slice_step_body(const Params& p, int64_t env, in
         uint32_t gnum = (uint32_t)(v.acc2 >> 32) + (uint32_t)(2 * (2 * cnt - (E - 1)));
         uint32_t sum_topo = (uint32_t)v.acc2 + (uint32_t)tl;
         v.acc2 = ((uint64_t)gnum << 32) | sum_topo;
-        v.acc3 += (uint64_t)node_cost(em_type(emA));
+        v.acc3 += (uint64_t)node_cost(em_type(pr.emA));
         v.s.acc = v.s.acc < 0xFFFF ? v.s.acc + 1 : 0xFFFF;
         if (v.s.rz == zA) v.s.intra = v.s.intra < 0xFFFF ? v.s.intra + 1 : 0xFFFF;
-        xsum_add(v.sum_lat, v.sum_cpu, v.sum_hi, sel_lat, sel_cpu, tl, v.s.rz != zA);
+        xsum_add(v.sum_lat, v.sum_cpu, v.sum_hi, sel_lat, pr.sel_cpu, tl, v.s.rz != zA);
         // increase_resources / increase_endpoint_latency (:674-677) and the same step's
         // decrease in next_request() (:1137-1143) -> the history counters advance
 #pragma unroll
@@ -406,11 +426,11 @@ __device__ __forceinline__ void slice_step_body(const Params& p, int64_t env, in
             const uint32_t edo = e == oA ? (v.ed[k] & ~(0x3FFu << 20)) | ((uint32_t)Mn << 20) : v.ed[k];
             const bool hit = e == ai;
             v.ed[k] = hit ? (edo & (0x3FFu << 20)) | ((uint32_t)Mn << 10) | (uint32_t)jn : edo;
-            v.olat[k] = hit ? (float)next_lat : v.olat[k];
-            v.ocpu[k] = hit ? (float)next_cpu : v.ocpu[k];
+            v.olat[k] = hit ? (float)pr.next_lat : v.olat[k];
+            v.ocpu[k] = hit ? (float)pr.next_cpu : v.ocpu[k];
         }
         v.s.penalty = 0;
-        reward = accept_reward(p, sel_lat, tl, sel_cpu, v.acc2, v.s.acc);
+        reward = accept_reward(p, sel_lat, tl, pr.sel_cpu, v.acc2, v.s.acc);
         v.last_r = reward;
     } else if (reject) {
         v.s.penalty = 1;
@@ -421,14 +441,9 @@ __device__ __forceinline__ void slice_step_body(const Params& p, int64_t env, in
     }
     v.total += reward;
 
-    // ---- next_request (:1131-1163), done (:472), outputs
+    // ---- next_request (:1131-1163), done (:472), auto-reset
     slice_next_request<W, TRACE, EPL>(p, env, lane, false, v);
-    const bool done = v.s.step == p.L;
-    if (lane == 0) {
-        if (reward_out) reward_out[env] = (float)reward;
-        if (rew64_out) rew64_out[env] = reward;
-        if (done_out) done_out[env] = (uint8_t)done;
-    }
+    done = v.s.step == p.L;
     if (done && p.auto_reset) {
         if (p.term_obs) slice_write_obs<W, EPL>(p, p.term_obs, env, lane, v);
         if (p.ep_stats && lane == 0)
@@ -441,19 +456,41 @@ __device__ __forceinline__ void slice_step_body(const Params& p, int64_t env, in
             if (e == ai || e == oA) p.edyn[eidx(p, env, e)] = v.ed[k];
         }
     }
-    if (obs_out) {
-        if constexpr (W == 16) {
-            // whole-line stores of the wave's 4 envs when all 4 are live
-            __shared__ float4 obs_stage[BLOCK / 64][8 * (16 * EPL + 1)];
-            const int wl = threadIdx.x & 63;
-            const int64_t env0 = env - wl / W;
-            if (env0 + 4 <= p.B) {
-                slice_write_obs_wave<EPL>(p, obs_out, env0, wl, v, obs_stage[threadIdx.x >> 6]);
-                return;
-            }
+    return reward;
+}
+// get_state() of the step's result: the wave's 4 envs as whole lines through LDS (W = 16), or
+// per env
+template <int W, int EPL>
+__device__ __forceinline__ void slice_obs(const Params& p, int64_t env, int lane, const SEnv<EPL>& v, float* obs_out) {
+    if constexpr (W == 16) {
+        // whole-line stores of the wave's 4 envs when all 4 are live
+        __shared__ float4 obs_stage[BLOCK / 64][8 * (16 * EPL + 1)];
+        const int wl = threadIdx.x & 63;
+        const int64_t env0 = env - wl / W;
+        if (env0 + 4 <= p.B) {
+            slice_write_obs_wave<EPL>(p, obs_out, env0, wl, v, obs_stage[threadIdx.x >> 6]);
+            return;
         }
-        slice_write_obs<W, EPL>(p, obs_out, env, lane, v);
     }
+    slice_write_obs<W, EPL>(p, obs_out, env, lane, v);
+}
+
+// one step() (:403-513) of the slice's env held in registers (the single-step kernel's order):
+// obs / reward / done of this step out (NULL = skip)
+template <int W, int EPL, bool TRACE, bool STORE_ED>
+__device__ __forceinline__ void slice_step_body(const Params& p, int64_t env, int lane, SEnv<EPL>& v, int a,
+                                                float* obs_out, float* reward_out, uint8_t* done_out,
+                                                double* rew64_out) {
+    const SPrep pr = slice_prep<W, EPL>(p, v, a);
+    slice_observe<EPL>(p, v);
+    bool done;
+    const double reward = slice_apply<W, EPL, TRACE, STORE_ED>(p, env, lane, v, pr, done);
+    if (lane == 0) {
+        if (reward_out) reward_out[env] = (float)reward;
+        if (rew64_out) rew64_out[env] = reward;
+        if (done_out) done_out[env] = (uint8_t)done;
+    }
+    if (obs_out) slice_obs<W, EPL>(p, env, lane, v, obs_out);
 }
 
 // step() (:403-513) fused with next_request(), get_state(), reward, done and auto-reset.
@@ -512,13 +549,26 @@ __global__ __launch_bounds__(BLOCK) void k_rollout_slice(Params p, int kind, int
     if (env >= p.B) return;
     SEnv<EPL> v;
     slice_load<W, EPL>(p, env, lane, v);
+    // the observed values live in registers for the whole launch: a step changes only the
+    // selected endpoint's (slice_apply), a reset sets them all (slice_reset)
+    slice_observe<EPL>(p, v);
     const int64_t obs_slot = p.B * (int64_t)p.R * 8;
+    int a = slice_policy<W, EPL>(p, env, lane, v, kind);
+    SPrep pr = slice_prep<W, EPL>(p, v, a);
     for (int k = 0; k < K; ++k) {
-        const int a = slice_policy<W, EPL>(p, env, lane, v, kind);
-        if (act_out && lane == 0) act_out[k * p.B + env] = a;
-        slice_step_body<W, EPL, false, false>(p, env, lane, v, a, p.obs ? p.obs + k * obs_slot : nullptr,
-                                               p.reward ? p.reward + k * p.B : nullptr,
-                                               p.done ? p.done + k * p.B : nullptr, nullptr);
+        bool done;
+        const double reward = slice_apply<W, EPL, false, false>(p, env, lane, v, pr, done);
+        const int ak = a;
+        if (k + 1 < K) {  // step k + 1's gathers, issued before step k's stores
+            a = slice_policy<W, EPL>(p, env, lane, v, kind);
+            pr = slice_prep<W, EPL>(p, v, a);
+        }
+        if (lane == 0) {
+            if (act_out) act_out[k * p.B + env] = ak;
+            if (p.reward) p.reward[k * p.B + env] = (float)reward;
+            if (p.done) p.done[k * p.B + env] = (uint8_t)done;
+        }
+        if (p.obs) slice_obs<W, EPL>(p, env, lane, v, p.obs + k * obs_slot);
     }
 #pragma unroll
     for (int k = 0; k < EPL; ++k) {
