@@ -25,6 +25,7 @@
 #include "lbk8s_common.h"
 #include "lbk8s_deepsets.h"
 #include "lbk8s_ds_train.h"
+#include "lbk8s_dqn.h"
 #include "lbk8s_slice.h"
 #include "lbk8s_tpe.h"
 #include "lbk8s_rollout.h"
@@ -800,6 +801,19 @@ int lb_rollout(void* state, const lb_config* cfg, int64_t num_envs, int32_t poli
     p.done = done_out;
     p.term_obs = terminal_obs_out;
     p.ep_stats = ep_stats_out;
+    if (g.W == 16 && g.EPL == 4 && p.E == 64 && p.R == 65 && g.NZW == 1) {  // config 4's shape, compile-time
+        const dim3 grid(slice_blocks(num_envs, 16));
+#define LB_SL64(RF_) hipLaunchKernelGGL((k_rollout_slice<16, 4, 64, 65, 1, RF_>), grid, dim3(BLOCK), 0, s, p, \
+                                        (int)policy, (int)steps, actions_out)
+        switch (p.reward_fn) {
+        case LB_REWARD_NAIVE: LB_SL64(LB_REWARD_NAIVE); break;
+        case LB_REWARD_LATENCY: LB_SL64(LB_REWARD_LATENCY); break;
+        case LB_REWARD_FAIRNESS: LB_SL64(LB_REWARD_FAIRNESS); break;
+        default: LB_SL64(LB_REWARD_MULTI); break;
+        }
+#undef LB_SL64
+        return check_launch();
+    }
     LB_DISPATCH_SLICE(g.W, g.EPL, {
         hipLaunchKernelGGL((k_rollout_slice<W, EPL>), dim3(slice_blocks(num_envs, W)), dim3(BLOCK), 0, s, p,
                            (int)policy, (int)steps, actions_out);
@@ -981,6 +995,59 @@ int lb_dqn_act(const float* frag, const float* obs, int64_t num_envs, int32_t nu
     p.ex_key0 = e.key0;
     p.ex_key1 = e.key1;
     ds_forward_launch<2>(p, (hipStream_t)stream);
+    return check_launch();
+}
+
+int lb_dqn_step(const float* frag, float* obs, int64_t num_envs, int32_t num_elements, const uint8_t* masks,
+                void* state, const lb_config* cfg, const lb_dqn_explore* ex, int32_t* actions_out,
+                float* next_obs_out, float* reward_out, uint8_t* done_out, float* terminal_obs_out,
+                double* ep_stats_out, int64_t slots, const int64_t* pos_in, int64_t* pos_out, float* rb_obs,
+                float* rb_next_obs, int64_t* rb_actions, float* rb_rewards, float* rb_dones, double* ep_sum,
+                double* ep_cnt, void* stream) {
+    if (int r = validate(cfg)) return r;
+    const Geo g = geometry(cfg, num_envs);
+    const int64_t simds = (int64_t)device_cus() * 4;
+    const bool fused = !g.tpe && g.W == 16 && g.EPL == 1 && num_elements <= 16 && (num_envs + DQN_P - 1) / DQN_P >= simds;
+    if (!fused) {  // the three launches
+        if (int rc = lb_dqn_act(frag, obs, num_envs, num_elements, masks, state, cfg, ex, actions_out, stream)) return rc;
+        if (int rc = lb_step(state, cfg, num_envs, actions_out, next_obs_out, reward_out, done_out, terminal_obs_out,
+                             ep_stats_out, nullptr, stream))
+            return rc;
+        return lb_replay_add(num_envs, num_elements * 8, slots, pos_in, pos_out, obs, next_obs_out, actions_out,
+                             reward_out, done_out, ep_stats_out, rb_obs, rb_next_obs, rb_actions, rb_rewards, rb_dones,
+                             ep_sum, ep_cnt, stream);
+    }
+    // (the three entry points' checks)
+    if (!frag || !obs || !state || !ex || !actions_out || !next_obs_out || !reward_out || !done_out || num_envs < 1)
+        return fail("lb_dqn_step: frag/obs/state/ex/actions/next_obs/reward/done NULL or num_envs < 1");
+    if (!ex->vstep_in || !ex->vstep_out || ex->vstep_in == ex->vstep_out || !ex->explore_out)
+        return fail("lb_dqn_explore: device words NULL (or vstep_in == vstep_out)");
+    if (cfg->rng_mode != LB_RNG_PHILOX) return fail("lb_dqn_step draws in Philox mode only");
+    const int32_t A = cfg->num_endpoints + (cfg->rejection_allowed ? 1 : 0);
+    if (num_elements != A) return fail("lb_dqn_step: num_elements must be the env's action count (R)");
+    if (slots < 1 || !pos_in || !pos_out || pos_in == pos_out || !rb_obs || !rb_next_obs || !rb_actions ||
+        !rb_rewards || !rb_dones || ((ep_sum || ep_cnt) && !(ep_sum && ep_cnt && ep_stats_out)))
+        return fail("replay buffers NULL (or pos_in == pos_out)");
+    Params e = make_params(state, cfg, num_envs);
+    e.obs = next_obs_out;
+    e.reward = reward_out;
+    e.done = done_out;
+    e.term_obs = terminal_obs_out;
+    e.ep_stats = ep_stats_out;
+    DSParams d{obs, frag, nullptr, nullptr, num_envs, num_elements, 1, 0, nullptr, nullptr, nullptr, nullptr,
+               actions_out, masks};
+    d.ex_on = 1;
+    d.ex = *ex;
+    d.ex_acc3 = e.acc3;
+    d.ex_sc = e.sc;
+    d.ex_env_offset = e.env_id_offset;
+    d.ex_key0 = e.key0;
+    d.ex_key1 = e.key1;
+    DQNReplay r{slots, num_elements * 2, pos_in, pos_out, reinterpret_cast<float4*>(obs),
+                reinterpret_cast<float4*>(rb_obs), reinterpret_cast<float4*>(rb_next_obs), rb_actions, rb_rewards,
+                rb_dones, ep_sum, ep_cnt};
+    const unsigned grid = ds_grid_spread((num_envs + DQN_P - 1) / DQN_P);
+    hipLaunchKernelGGL(k_dqn_step, dim3(grid), dim3(DS_BLOCK), 0, (hipStream_t)stream, d, e, r);
     return check_launch();
 }
 

@@ -331,6 +331,101 @@ __device__ __forceinline__ void store_rows(float* plane, const float (&h)[P * TS
         }
 }
 
+// one wave iteration's P envs: the observation -> layer-1 B fragments and its set-wise max
+template <int TS, int P, int MODE>
+__device__ __forceinline__ void ds_group_obs(const DSParams& p, int64_t env0, int col, int grp, int R,
+                                             float (&h0)[P * TS][2], float (&m0)[2]) {
+    constexpr bool TRAIN = MODE == 1;
+    // obs -> layer-1 B fragments: k-step kk holds feature 4kk + grp of set element col
+#pragma unroll
+    for (int s = 0; s < P; ++s) {
+        const bool live = env0 + s < p.B;
+        const float* x = p.obs + (env0 + s) * (int64_t)R * 8;
+#pragma unroll
+        for (int t = 0; t < TS; ++t) {
+            const int row = 16 * t + col;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) h0[s * TS + t][kk] = (live && row < R) ? x[row * 8 + 4 * kk + grp] : 0.f;
+        }
+    }
+    set_max_batched<TS, P, 2>(h0, m0, col, R);
+    if (TRAIN) store_obs_max<TS, P>(m0, col, grp, env0, p.B, p.setvec);
+}
+
+// one wave iteration's P envs: the actor (or Q network) Eq(8->64) ReLU Eq(64->64) ELU Eq(64->1);
+// logits / training rows / the masked greedy action (ARGMAX: lane s < P returns env0 + s's)
+template <int TS, int P, int MODE>
+__device__ __forceinline__ int32_t ds_group_actor(const DSParams& p, const float* W, int lane, int64_t env0, int col,
+                                                  int grp, int R, const float (&h0)[P * TS][2], const float (&m0)[2]) {
+    constexpr bool TRAIN = MODE == 1, ARGMAX = MODE == 2;
+    int32_t act = -1;
+    float h1[P * TS][16], m1[16], h2[P * TS][16], m2[16];
+    // ---- actor: Eq(8->64) ReLU Eq(64->64) ELU Eq(64->1)
+    if (p.actor) {
+        eq_layer<TS, P, 2, 1>(W + DS_A1L, W + DS_A1G, h0, m0, h1, lane);
+        if (TRAIN) store_rows<TS, P>(p.save_actor, h1, env0, p.B, R, col, grp);
+        if (TRAIN) set_max_store<TS, P, 16>(h1, m1, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX1A, LB_DSV_ID1A);
+        else set_max_batched<TS, P, 16>(h1, m1, col, R);
+        eq_layer<TS, P, 16, 2>(W + DS_A2L, W + DS_A2G, h1, m1, h2, lane);
+        if (TRAIN) store_rows<TS, P>(p.save_actor + p.B * (int64_t)R * 64, h2, env0, p.B, R, col, grp);
+        if (TRAIN) set_max_store<TS, P, 16>(h2, m2, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX2A, LB_DSV_ID2A);
+        else set_max_batched<TS, P, 16>(h2, m2, col, R);
+        // layer 3 (64 -> 1) on the VALU: a 16-row output tile would use 1/16 of an MFMA.
+        // Lane (col, grp) dots its 16 features with Lambda3 / -Gamma3 (row 0 of the
+        // fragments: column 0 of its row group), then the 4 row groups are summed.
+        const float* L = W + DS_A3L + 16 * grp;
+        const float* G = W + DS_A3G + 16 * grp;
+        float gl = 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) gl += G[k * 64] * m2[k];
+        gl += __shfl_xor(gl, 16);
+        gl += __shfl_xor(gl, 32);
+        float best[P], brow[P];  // this lane's first masked maximum per env (argmax mode)
+#pragma unroll
+        for (int s = 0; s < P; ++s) {
+            const float init = from_col_dyn<P>(gl, s);
+            best[s] = -INFINITY;
+            brow[s] = 1e9f;
+#pragma unroll
+            for (int t = 0; t < TS; ++t) {
+                float v = 0.f;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) v += L[k * 64] * h2[s * TS + t][k];
+                v += __shfl_xor(v, 16);
+                v += __shfl_xor(v, 32);
+                const int row = 16 * t + col;
+                const bool live = row < R && env0 + s < p.B;
+                if (grp == 0 && live && p.logits) p.logits[(env0 + s) * R + row] = init + v;
+                if (ARGMAX && live) {
+                    const float q = (!p.masks || p.masks[(env0 + s) * R + row]) ? init + v : -1e8f;
+                    if (q > best[s]) {
+                        best[s] = q;
+                        brow[s] = (float)row;
+                    }
+                }
+            }
+        }
+        if (ARGMAX) {
+            // over the 16 columns: the max, then the smallest row attaining it
+            float m[P], c[P];
+#pragma unroll
+            for (int s = 0; s < P; ++s) m[s] = best[s];
+            row_reduce<true>(m);
+#pragma unroll
+            for (int s = 0; s < P; ++s) c[s] = best[s] == m[s] ? -brow[s] : -1e9f;
+            row_reduce<true>(c);
+            if (lane < P && env0 + lane < p.B) {
+                float r = -c[0];
+#pragma unroll
+                for (int s = 1; s < P; ++s) r = lane == s ? -c[s] : r;
+                p.actions[env0 + lane] = (int32_t)r;
+                act = (int32_t)r;
+            }
+        }
+    }
+    return act;
+}
+
 // MODE 0: logits / value; 1: training forward (TRAIN: activations, psi mean); 2: Q values
 // and the masked greedy action (ARGMAX; actor only)
 template <int TS, int P, int MODE>
@@ -354,86 +449,10 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
     const int64_t groups = (p.B + P - 1) / P;
     for (int64_t gi = wave; gi < groups; gi += nwaves) {
         const int64_t env0 = gi * P;
-        // obs -> layer-1 B fragments: k-step kk holds feature 4kk + grp of set element col
-        float h0[P * TS][2];
-#pragma unroll
-        for (int s = 0; s < P; ++s) {
-            const bool live = env0 + s < p.B;
-            const float* x = p.obs + (env0 + s) * (int64_t)R * 8;
-#pragma unroll
-            for (int t = 0; t < TS; ++t) {
-                const int row = 16 * t + col;
-#pragma unroll
-                for (int kk = 0; kk < 2; ++kk) h0[s * TS + t][kk] = (live && row < R) ? x[row * 8 + 4 * kk + grp] : 0.f;
-            }
-        }
-        float m0[2];
-        set_max_batched<TS, P, 2>(h0, m0, col, R);
-        if (TRAIN) store_obs_max<TS, P>(m0, col, grp, env0, p.B, p.setvec);
-
+        float h0[P * TS][2], m0[2];
+        ds_group_obs<TS, P, MODE>(p, env0, col, grp, R, h0, m0);
+        ds_group_actor<TS, P, MODE>(p, W, lane, env0, col, grp, R, h0, m0);
         float h1[P * TS][16], m1[16], h2[P * TS][16], m2[16];
-        // ---- actor: Eq(8->64) ReLU Eq(64->64) ELU Eq(64->1)
-        if (p.actor) {
-            eq_layer<TS, P, 2, 1>(W + DS_A1L, W + DS_A1G, h0, m0, h1, lane);
-            if (TRAIN) store_rows<TS, P>(p.save_actor, h1, env0, p.B, R, col, grp);
-            if (TRAIN) set_max_store<TS, P, 16>(h1, m1, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX1A, LB_DSV_ID1A);
-            else set_max_batched<TS, P, 16>(h1, m1, col, R);
-            eq_layer<TS, P, 16, 2>(W + DS_A2L, W + DS_A2G, h1, m1, h2, lane);
-            if (TRAIN) store_rows<TS, P>(p.save_actor + p.B * (int64_t)R * 64, h2, env0, p.B, R, col, grp);
-            if (TRAIN) set_max_store<TS, P, 16>(h2, m2, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX2A, LB_DSV_ID2A);
-            else set_max_batched<TS, P, 16>(h2, m2, col, R);
-            // layer 3 (64 -> 1) on the VALU: a 16-row output tile would use 1/16 of an MFMA.
-            // Lane (col, grp) dots its 16 features with Lambda3 / -Gamma3 (row 0 of the
-            // fragments: column 0 of its row group), then the 4 row groups are summed.
-            const float* L = W + DS_A3L + 16 * grp;
-            const float* G = W + DS_A3G + 16 * grp;
-            float gl = 0.f;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) gl += G[k * 64] * m2[k];
-            gl += __shfl_xor(gl, 16);
-            gl += __shfl_xor(gl, 32);
-            float best[P], brow[P];  // this lane's first masked maximum per env (argmax mode)
-#pragma unroll
-            for (int s = 0; s < P; ++s) {
-                const float init = from_col_dyn<P>(gl, s);
-                best[s] = -INFINITY;
-                brow[s] = 1e9f;
-#pragma unroll
-                for (int t = 0; t < TS; ++t) {
-                    float v = 0.f;
-#pragma unroll
-                    for (int k = 0; k < 16; ++k) v += L[k * 64] * h2[s * TS + t][k];
-                    v += __shfl_xor(v, 16);
-                    v += __shfl_xor(v, 32);
-                    const int row = 16 * t + col;
-                    const bool live = row < R && env0 + s < p.B;
-                    if (grp == 0 && live && p.logits) p.logits[(env0 + s) * R + row] = init + v;
-                    if (ARGMAX && live) {
-                        const float q = (!p.masks || p.masks[(env0 + s) * R + row]) ? init + v : -1e8f;
-                        if (q > best[s]) {
-                            best[s] = q;
-                            brow[s] = (float)row;
-                        }
-                    }
-                }
-            }
-            if (ARGMAX) {
-                // over the 16 columns: the max, then the smallest row attaining it
-                float m[P], c[P];
-#pragma unroll
-                for (int s = 0; s < P; ++s) m[s] = best[s];
-                row_reduce<true>(m);
-#pragma unroll
-                for (int s = 0; s < P; ++s) c[s] = best[s] == m[s] ? -brow[s] : -1e9f;
-                row_reduce<true>(c);
-                if (lane < P && env0 + lane < p.B) {
-                    float r = -c[0];
-#pragma unroll
-                    for (int s = 1; s < P; ++s) r = lane == s ? -c[s] : r;
-                    p.actions[env0 + lane] = (int32_t)r;
-                }
-            }
-        }
         if (ARGMAX || !p.critic) continue;
 
         // ---- critic: psi = Eq ELU Eq ELU Eq, mean over the set, rho = Linear ELU Linear

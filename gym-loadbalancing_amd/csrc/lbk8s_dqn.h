@@ -1,0 +1,108 @@
+// lbk8s_dqn.h — lb_dqn_step: one DQN vector step (envs/dqn_deepset.py:122-174) in ONE launch.
+//
+// The device DQN loop's vector step was three launches: lb_dqn_act (the explore decision, then
+// the greedy action of the Q network's fused forward or every env's random action), lb_step
+// (the env step) and lb_replay_add (the replay write, obs <- next obs, the finished episodes'
+// sums).  Each env's chain -- its Q values, its action, its step, its replay row -- touches no
+// other env, so one wave carries it through for four envs at a time: the forward's P = 4 sets
+// of a wave iteration are exactly the four 16-lane env slices of the slice layout's step kernel
+// (W = 16, one endpoint per lane: the env layout of E <= 16 at fewer than 32,768 envs).  At
+// config 5 (4096 envs) the step and replay kernels were ~5 us each of mostly launch ramp and
+// tail (profiles/r03_dqn_kernel_stats_setgrads.csv); here they follow the forward inside the
+// same waves.  Same functions, same order per env: bit for bit the three launches
+// (tests/test_gpu_dqn_step.py).
+#pragma once
+
+#include "lbk8s_deepsets.h"
+#include "lbk8s_slice.h"
+
+namespace lbk {
+
+constexpr int DQN_P = 4;  // envs per wave iteration (the Q forward's P, the slice step's envs per wave)
+
+struct DQNReplay {  // lb_replay_add's buffers
+    int64_t slots;
+    int f4;  // float4s per observation
+    const int64_t* pos_in;
+    int64_t* pos_out;
+    float4* obs;  // [B][f4] the step's input observations; <- the next observations
+    float4* rb_obs;
+    float4* rb_next_obs;
+    int64_t* rb_actions;
+    float* rb_rewards;
+    float* rb_dones;
+    double* ep_sum;  // [B] or NULL
+    double* ep_cnt;
+};
+
+// d: the Q forward (lb_dqn_act's DSParams: obs, the actor-only weight image, masks, actions,
+// the explore struct); e: the env (lb_step's Params: obs = the next observations, reward,
+// done, terminal obs, ep_stats); r: the replay buffer.
+__global__ __launch_bounds__(DS_BLOCK, 2) void k_dqn_step(DSParams d, Params e, DQNReplay r) {
+    constexpr int P = DQN_P, NWB = DS_BLOCK / 64;
+    const int64_t t = *d.ex.vstep_in;
+    const int64_t pos = *r.pos_in;
+    const bool explore = dqn_explores(d.ex, t);  // (:127, uniform over the launch)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *d.ex.explore_out = explore ? 1 : 0;
+        *d.ex.vstep_out = t + 1;
+        *r.pos_out = (pos + 1) % r.slots;
+    }
+    __shared__ __attribute__((aligned(16))) float W[DS_C1L];  // the Q network's fragments
+    if (!explore) {
+        for (int i = threadIdx.x * 4; i < DS_C1L; i += DS_BLOCK * 4)
+            *reinterpret_cast<float4*>(W + i) = *reinterpret_cast<const float4*>(d.wfrag + i);
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63;
+    // wave-major numbering, as k_deepsets_fwd: fewer groups than waves put one wave per SIMD
+    const int64_t wave = (int64_t)(threadIdx.x >> 6) * gridDim.x + blockIdx.x;
+    const int64_t nwaves = (int64_t)gridDim.x * NWB;
+    const int R = d.R, col = lane & 15, grp = lane >> 4;
+    const int64_t groups = (d.B + P - 1) / P, n4 = e.B * r.f4;
+    const int s = lane >> 4, l16 = lane & 15;
+    for (int64_t gi = wave; gi < groups; gi += nwaves) {
+        const int64_t env0 = gi * P;
+        // the greedy actions of the group's envs (lane s holds env0 + s's; :134-142)
+        int32_t act = -1;
+        if (!explore) {
+            float h0[P][2], m0[2];
+            ds_group_obs<1, P, 2>(d, env0, col, grp, R, h0, m0);
+            act = ds_group_actor<1, P, 2>(d, W, lane, env0, col, grp, R, h0, m0);
+        }
+        const int32_t ag = __shfl(act, s);
+        // the env step: lanes 16 s .. 16 s + 15 step env env0 + s (k_step_slice<16, 1>'s body)
+        const int64_t env = env0 + s;
+        int a = 0;
+        if (env < e.B) {
+            SEnv<1> v;
+            slice_load<16, 1>(e, env, l16, v);
+            a = explore ? random_action(e, env, v.acc3, v.s.step) : ag;  // (exploring: :128-131)
+            if (explore && l16 == 0) d.actions[env] = a;
+            slice_step_body<16, 1, false, true, NWB>(e, env, l16, v, a, e.obs, e.reward, e.done, e.rew64);
+            if (l16 == 0) slice_store_scalars<1>(e, env, v);
+        }
+        // the group's replay rows (lb_replay_add's), once the step's outputs have landed
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int64_t hi = (env0 + P < e.B ? env0 + P : e.B) * r.f4;
+        const float4* nxo = reinterpret_cast<const float4*>(e.obs);
+        for (int64_t i = env0 * r.f4 + lane; i < hi; i += 64) {
+            const float4 o = r.obs[i], nx = nxo[i];
+            r.rb_obs[pos * n4 + i] = o;
+            r.rb_next_obs[pos * n4 + i] = nx;
+            r.obs[i] = nx;
+        }
+        if (l16 == 0 && env < e.B) {  // (the lane that wrote the env's reward, done and stats row)
+            const bool dn = e.done[env] != 0;
+            r.rb_actions[pos * e.B + env] = a;
+            r.rb_rewards[pos * e.B + env] = e.reward[env];
+            r.rb_dones[pos * e.B + env] = dn ? 1.f : 0.f;
+            if (r.ep_sum && dn) {
+                r.ep_sum[env] += e.ep_stats[env * LB_ST_K];
+                r.ep_cnt[env] += 1.0;
+            }
+        }
+    }
+}
+
+}  // namespace lbk

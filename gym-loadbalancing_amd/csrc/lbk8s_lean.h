@@ -694,6 +694,7 @@ __global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p
     auto iter = [&](const int k) {
         LB_LTL(k, 0);
         // issue priority by progress (k_rollout_img): a wave behind the others goes first
+#ifndef LB_LEAN_NOPRIO
         {
             const int pl = 3 - (4 * k) / K;
             if (pl >= 3) __builtin_amdgcn_s_setprio(3);
@@ -701,6 +702,7 @@ __global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p
             else if (pl == 1) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(0);
         }
+#endif
         const int a_k = (int)(pr.arz & 0xFFu);
         v.s0 += 1;  // step (<= L: the episode ends there)
         const bool done = (int)(v.s0 & 0xFFFF) == p.L;  // (:472)

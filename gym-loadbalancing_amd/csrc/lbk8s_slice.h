@@ -460,11 +460,11 @@ __device__ __forceinline__ double slice_apply(const Params& p, int64_t env, int 
 }
 // get_state() of the step's result: the wave's 4 envs as whole lines through LDS (W = 16), or
 // per env
-template <int W, int EPL>
+template <int W, int EPL, int NWB = BLOCK / 64>  // NWB: waves per block (the LDS stage has one region per wave)
 __device__ __forceinline__ void slice_obs(const Params& p, int64_t env, int lane, const SEnv<EPL>& v, float* obs_out) {
     if constexpr (W == 16) {
         // whole-line stores of the wave's 4 envs when all 4 are live
-        __shared__ float4 obs_stage[BLOCK / 64][8 * (16 * EPL + 1)];
+        __shared__ float4 obs_stage[NWB][8 * (16 * EPL + 1)];
         const int wl = threadIdx.x & 63;
         const int64_t env0 = env - wl / W;
         if (env0 + 4 <= p.B) {
@@ -477,7 +477,7 @@ __device__ __forceinline__ void slice_obs(const Params& p, int64_t env, int lane
 
 // one step() (:403-513) of the slice's env held in registers (the single-step kernel's order):
 // obs / reward / done of this step out (NULL = skip)
-template <int W, int EPL, bool TRACE, bool STORE_ED>
+template <int W, int EPL, bool TRACE, bool STORE_ED, int NWB = BLOCK / 64>
 __device__ __forceinline__ void slice_step_body(const Params& p, int64_t env, int lane, SEnv<EPL>& v, int a,
                                                 float* obs_out, float* reward_out, uint8_t* done_out,
                                                 double* rew64_out) {
@@ -490,7 +490,7 @@ __device__ __forceinline__ void slice_step_body(const Params& p, int64_t env, in
         if (rew64_out) rew64_out[env] = reward;
         if (done_out) done_out[env] = (uint8_t)done;
     }
-    if (obs_out) slice_obs<W, EPL>(p, env, lane, v, obs_out);
+    if (obs_out) slice_obs<W, EPL, NWB>(p, env, lane, v, obs_out);
 }
 
 // step() (:403-513) fused with next_request(), get_state(), reward, done and auto-reset.
@@ -542,8 +542,17 @@ __device__ __forceinline__ int slice_policy(const Params& p, int64_t env, int la
 // lb_rollout: K steps per launch under an on-device policy, the env state held in
 // registers between steps; step k's obs / reward / done go to slot k of the caller's
 // buffers.  Bit for bit K x (lb_policy + lb_step) (tests/test_gpu_api.py).
-template <int W, int EPL>
-__global__ __launch_bounds__(BLOCK) void k_rollout_slice(Params p, int kind, int K, int32_t* act_out) {
+// ET / RT / NZWT / RF > 0 (>= 0 for RF): the shape is a compile-time constant (config 4's E = 64,
+// R = 65, N <= 32, multi reward): a local copy of the parameters with those fields fixed lets
+// every loop over the endpoints, rows and node words unroll and the reward's other kinds fold
+// away, which took the per-step uniform values the compiler kept in (spilled) SGPRs down.
+template <int W, int EPL, int ET = 0, int RT = 0, int NZWT = 0, int RF = -1>
+__global__ __launch_bounds__(BLOCK) void k_rollout_slice(Params pa, int kind, int K, int32_t* act_out) {
+    Params p = pa;
+    if (ET > 0) p.E = ET;
+    if (RT > 0) p.R = RT;
+    if (NZWT > 0) p.NZW = NZWT;
+    if (RF >= 0) p.reward_fn = RF;
     const int lane = threadIdx.x % W;
     const int64_t env = (int64_t)blockIdx.x * (BLOCK / W) + threadIdx.x / W;
     if (env >= p.B) return;

@@ -14,7 +14,7 @@ _PRODUCT_LIB = LIB_PATH
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
 # csrc/Makefile's SRCS, in order: the library embeds the SHA-256 of their concatenation
 SOURCES = ("lbk8s.hip", "lbk8s_common.h", "lbk8s_slice.h", "lbk8s_tpe.h", "lbk8s_rollout.h", "lbk8s_lean.h",
-           "lbk8s_deepsets.h", "lbk8s_ds_train.h", "../../include/lbk8s.h")
+           "lbk8s_deepsets.h", "lbk8s_ds_train.h", "lbk8s_dqn.h", "../../include/lbk8s.h")
 ABI_VERSION = 9
 
 LB_REWARD = {"naive": 0, "latency": 1, "fairness": 2, "multi": 3}
@@ -175,6 +175,8 @@ def lib():
     L.lb_episode_log.argtypes = [i64, vp, vp, vp, vp, vp, vp, vp, i64, vp, i64, vp, vp]
     L.lb_reward64.argtypes = [vp, cfgp, i64, C.POINTER(C.c_void_p)]
     L.lb_dqn_act.argtypes = [vp, vp, i64, i32, vp, vp, cfgp, C.POINTER(LBDQNExploreC), vp, vp]
+    L.lb_dqn_step.argtypes = [vp, vp, i64, i32, vp, vp, cfgp, C.POINTER(LBDQNExploreC), vp, vp, vp, vp, vp, vp,
+                              i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.lb_dqn_head.argtypes = [vp, vp, vp, vp, vp, i64, i32, C.c_float, vp, vp, vp, vp, vp]
     L.lb_replay_sample.argtypes = [i64, i32, i64, i32, C.c_uint64] + [vp] * 12 + [vp]
     L.lb_ds_set_grads.argtypes = [vp, vp, vp, i64, i32, vp, vp]
@@ -183,7 +185,7 @@ def lib():
               "lb_get_field", "lb_get_stats", "lb_status", "lb_ds_pack", "lb_ds_forward",
               "lb_ds_train_forward", "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax",
               "lb_replay_add", "lb_ppo_head", "lb_episode_log", "lb_dqn_act", "lb_dqn_head",
-              "lb_replay_sample", "lb_ds_set_grads"):
+              "lb_replay_sample", "lb_ds_set_grads", "lb_dqn_step"):
         getattr(L, f).restype = C.c_int
     v = L.lb_abi_version()
     if v != ABI_VERSION and product:
@@ -213,4 +215,4 @@ EXPORTED_SYMBOLS = ("lb_abi_version", "lb_last_error", "lb_validate_config", "lb
                     "lb_status", "lb_ds_pack", "lb_ds_forward", "lb_ds_train_forward",
                     "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax", "lb_replay_add", "lb_ppo_head",
                     "lb_episode_log", "lb_dqn_act", "lb_dqn_head", "lb_replay_sample", "lb_ds_set_grads",
-                    "lb_rollout_kernel", "lb_source_hash", "lb_reward64")
+                    "lb_rollout_kernel", "lb_source_hash", "lb_reward64", "lb_dqn_step")

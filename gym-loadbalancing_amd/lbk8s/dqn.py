@@ -264,11 +264,10 @@ class DQN_DeepSets:
         """One vector step with the explore decision on the device: [random actions | greedy
         actions from the packed image] in one launch (lb_dqn_act), the env step, lb_replay_add.
         The q image (self._qfrag) is packed by the caller."""
-        env = self.env
-        env.dqn_act(self._qfrag, obs, masks, self._ex[parity], self._act)
-        env.step_device(self._act, obs_out=self._next_obs, reward_out=self._rew, done_out=self._done_u8)
-        self.rb.add_fused(obs, self._next_obs, self._act, self._rew, self._done_u8, env.ep_stats,
-                          self._ep_sum, self._ep_cnt, parity)
+        env, pp = self.env, self.rb.pos_pp.data_ptr()
+        # (lb_dqn_step: the three in one launch at config 5's shape, bit for bit)
+        env.dqn_step(self._qfrag, obs, masks, self._ex[parity], self._act, self._next_obs, self._rew, self._done_u8,
+                     self.rb, pp + 8 * parity, pp + 8 * (1 - parity), self._ep_sum, self._ep_cnt)
 
     def _sample_dev(self, parity):
         """lb_replay_sample into the train step's fixed buffers; the counter is the vector step

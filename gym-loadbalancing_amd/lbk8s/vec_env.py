@@ -486,6 +486,20 @@ class LBVecEnv:
                                          self._stream()))
         return out
 
+    def dqn_step(self, frag, obs, masks, ex, actions, next_obs, reward, done, rb, pos_in, pos_out, ep_sum, ep_cnt):
+        """lb_dqn_step: one DQN vector step -- dqn_act, step_device(actions, next_obs, reward, done)
+        and the replay write (lb_replay_add into rb at the device slot *pos_in, obs <- next_obs,
+        finished-episode sums) -- in one launch where the shape allows it (config 5's 4096 envs),
+        else as those three launches; bit for bit the same either way."""
+        R = obs.shape[1]
+        _native.check(self._L.lb_dqn_step(
+            frag.data_ptr(), obs.data_ptr(), self.num_envs, R, self._ptr(masks), self._ptr(self.state),
+            C.byref(self._c), C.byref(ex), self._ptr(actions), self._ptr(next_obs), self._ptr(reward), self._ptr(done),
+            self._ptr(self.terminal_obs), self._ptr(self.ep_stats), rb.size, pos_in, pos_out, rb.obs.data_ptr(),
+            rb.next_obs.data_ptr(), rb.actions.data_ptr(), rb.rewards.data_ptr(), rb.dones.data_ptr(),
+            self._ptr(ep_sum), self._ptr(ep_cnt), self._stream()))
+        return actions
+
     def field(self, name):
         """Env attribute as a float64 device tensor: (B, E) or (B,)."""
         shape = (self.num_envs,) if name in _native.PER_ENV_FIELDS else (self.num_envs, self.cfg.num_endpoints)

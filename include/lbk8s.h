@@ -295,6 +295,19 @@ int lb_dqn_act(const float* frag, const float* obs, int64_t num_envs, int32_t nu
                const void* state, const lb_config* cfg, const lb_dqn_explore* ex, int32_t* actions_out,
                void* stream);
 
+/* One DQN vector step (dqn_deepset.py:122-174) = lb_dqn_act; lb_step(actions_out, next_obs_out,
+ * reward_out, done_out, terminal_obs_out, ep_stats_out); lb_replay_add(obs, next_obs_out, ...)
+ * with the same arguments, bit for bit, in ONE launch where the shape allows it (the env in the
+ * slice layout with 16 lanes per env, i.e. E <= 16 below 32,768 envs; R <= 16; at least four
+ * envs per SIMD: config 5's 4096 envs): each wave takes four envs through the Q forward, the
+ * step and the replay write.  Other shapes run the three launches. */
+int lb_dqn_step(const float* frag, float* obs, int64_t num_envs, int32_t num_elements, const uint8_t* masks,
+                void* state, const lb_config* cfg, const lb_dqn_explore* ex, int32_t* actions_out,
+                float* next_obs_out, float* reward_out, uint8_t* done_out, float* terminal_obs_out,
+                double* ep_stats_out, int64_t slots, const int64_t* pos_in, int64_t* pos_out, float* rb_obs,
+                float* rb_next_obs, int64_t* rb_actions, float* rb_rewards, float* rb_dones, double* ep_sum,
+                double* ep_cnt, void* stream);
+
 /* DQN loss head (dqn_deepset.py:180-187): per sample td = r + gamma max q_next (1 - done),
  * sq_err_out = (td - q[a])^2 (mean = F.mse_loss) and dq_out = d mean / d q (2 (q[a] - td) /
  * M at column a, 0 elsewhere); td_out / old_out (may be NULL) the TD target and q[a].
