@@ -94,6 +94,35 @@ __device__ __forceinline__ U4 draw_o(const Params& p, int64_t env, uint32_t epis
     LB_GUARD_V(hi);
     return philox(c0, episode, slot, dom | hi, k0, k1);
 }
+// two blocks with one key schedule (the request's X and I blocks of a step: same counter but
+// the domain word): the 10 rounds' key additions are issued once for both, and the two
+// independent chains interleave.  Each block equals draw_o's.
+__device__ __forceinline__ void draw2_o(const Params& p, int64_t env, uint32_t episode, uint32_t slot, uint32_t dom_a,
+                                        uint32_t dom_b, U4& a, U4& b) {
+    uint32_t k0 = p.key0, k1 = p.key1;
+    LB_GUARD_S(k0);
+    LB_GUARD_S(k1);
+    const uint64_t gid = (uint64_t)(p.env_id_offset + env);
+    uint32_t c0 = (uint32_t)gid, hi = (uint32_t)(gid >> 32) << 8;
+    LB_GUARD_V(c0);
+    LB_GUARD_V(hi);
+    uint32_t a0 = c0, a1 = episode, a2 = slot, a3 = dom_a | hi;
+    uint32_t b0 = c0, b1 = episode, b2 = slot, b3 = dom_b | hi;
+#pragma unroll
+    for (int i = 0; i < LB_PHILOX_ROUNDS; ++i) {  // (philox()'s round, twice)
+        const uint64_t pa0 = (uint64_t)0xD2511F53u * a0, pa1 = (uint64_t)0xCD9E8D57u * a2;
+        const uint64_t pb0 = (uint64_t)0xD2511F53u * b0, pb1 = (uint64_t)0xCD9E8D57u * b2;
+        const uint32_t na0 = (uint32_t)(pa1 >> 32) ^ a1 ^ k0, na2 = (uint32_t)(pa0 >> 32) ^ a3 ^ k1;
+        const uint32_t nb0 = (uint32_t)(pb1 >> 32) ^ b1 ^ k0, nb2 = (uint32_t)(pb0 >> 32) ^ b3 ^ k1;
+        a0 = na0; a1 = (uint32_t)pa1; a2 = na2; a3 = (uint32_t)pa0;
+        b0 = nb0; b1 = (uint32_t)pb1; b2 = nb2; b3 = (uint32_t)pb0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    a = {a0, a1, a2, a3};
+    b = {b0, b1, b2, b3};
+}
+
 template <int KIND>
 __device__ __forceinline__ int lean_policy(const Params& p, int64_t env, const TEnv& tv, const uint32_t (&em)[TPE_E],
                                            const uint32_t (&ed)[TPE_E]) {
@@ -277,7 +306,7 @@ __device__ __forceinline__ void lean_write_record(const Params& p, int64_t env, 
 // staged record: 0..7 emeta, 8..20 scalars, 24..39 lat0; the rows land on words 0..31 and the
 // lem words on 32..39, which the env's lane then overwrites with the reject row and the
 // request block (it reads them first).
-template <int ET, int RT>
+template <int ET, int RT, int NG>  // NG: at most NG envs in grp (the ctz walk stops there)
 __device__ __forceinline__ void lean_restart_group(const Params& p, const LDims<ET, RT>& d, uint32_t* wimg,
                                                    uint64_t grp, int lane, bool mine, LEnv& v,
                                                    uint32_t (&em)[TPE_E], uint32_t (&ed)[TPE_E], uint32_t* me) {
@@ -314,7 +343,7 @@ __device__ __forceinline__ void lean_restart_group(const Params& p, const LDims<
     {
         uint64_t m = grp;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < NG; ++i) {
             const int b = m ? (int)__builtin_ctzll(m) : -1;
             if (g == i) el = b;
             m &= m - 1;
@@ -355,13 +384,16 @@ __device__ __forceinline__ void lean_restart_group(const Params& p, const LDims<
 }
 
 // lane -> (env, record chunk) of the record fetch: lanes 10 i .. 10 i + 9 fetch the record
-// of the i-th lowest env of m (i < 6); returns the env's lane or -1
+// of the i-th lowest env of m (i < NJ <= 6: the callers' groups hold at most NJ envs);
+// returns the env's lane or -1
+template <int NJ>
 __device__ __forceinline__ int rec_fetch_env(uint64_t m, int lane, int& chunk) {
+    static_assert(NJ <= 6, "64 lanes: 6 records of 10 chunks");
     const int i = lane / 10;
     chunk = lane - 10 * i;
     int el = -1;
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
+    for (int j = 0; j < NJ; ++j) {
         const int b = m ? (int)__builtin_ctzll(m) : -1;
         if (i == j) el = b;
         m &= m - 1;
@@ -614,7 +646,7 @@ __global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p
         const uint64_t mn = __ballot((int)(steps_done + 1) == p.L);
         int chunk, ln = lane;
         LB_GUARD_V(ln);  // (recomputed per step: hoisted, the lane's chunk and slot spilled)
-        const int el = rec_fetch_env(mn, ln, chunk);
+        const int el = rec_fetch_env<FAST>(mn, ln, chunk);
         const uint32_t w0 = rec_off + (uint32_t)env0 * RO_REC_BYTES;
         qn = buf_ld_u128(blob, el >= 0 ? w0 + (uint32_t)el * RO_REC_BYTES + 16u * chunk : w0);
     };
@@ -656,8 +688,9 @@ __global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p
         between(0);
         asm volatile("" ::: "memory");
         const uint32_t episode = (uint32_t)(v.acc3 >> 32), slot = (uint32_t)(step + 1);
-        const U4 wx = draw_o(p, env, episode, slot, D_REQ_X);
-        asm volatile("" ::"v"(wx.x), "v"(wx.y), "v"(wx.z), "v"(wx.w) : "memory");
+        U4 wx, wi;
+        draw2_o(p, env, episode, slot, D_REQ_X, D_REQ_I, wx, wi);
+        asm volatile("" ::"v"(wx.x), "v"(wx.y), "v"(wx.z), "v"(wx.w), "v"(wi.x), "v"(wi.y) : "memory");
         between(1);
         asm volatile("" ::: "memory");
         const double x1 = p.inv_rate * std_exp(wx.x, wx.y);
@@ -671,7 +704,6 @@ __global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p
         asm volatile("" ::"v"(r.arr), "v"(r.dt) : "memory");
         between(3);
         asm volatile("" ::: "memory");
-        const U4 wi = draw_o(p, env, episode, slot, D_REQ_I);
         const int rr = (int)bounded(wi.x, 7), n = (int)bounded(wi.y, (uint32_t)p.N);
         const uint64_t word = (NZW > 1 && n >= 32) ? v.nz1 : v.nz0;
         const uint32_t rz = (uint32_t)((word >> (2 * (n & 31))) & 3);
@@ -731,7 +763,7 @@ __global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p
                                       (uint32_t)((env0 + tel) * P + pc) * 16u);
                 const bool mine = done && ((grp >> lane) & 1);
                 int chunk;
-                const int rl = rec_fetch_env(grp, lane, chunk);
+                const int rl = rec_fetch_env<FAST>(grp, lane, chunk);
                 uint4* dst = reinterpret_cast<uint4*>(wimg + rl * IMG_W + 4 * chunk);
                 wave_lds_sync();  // (the rows are read before the records overwrite them)
                 if (pre) {
@@ -751,7 +783,7 @@ __global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p
                                  blob, o + 32u);
                 }
                 wave_lds_sync();
-                lean_restart_group(p, d, wimg, grp, lane, mine, v, em, ed, me);
+                lean_restart_group<ET, RT, FAST>(p, d, wimg, grp, lane, mine, v, em, ed, me);
                 if (mine) {
                     new_episode = true;
                     l0off = rec_off + envi * RO_REC_BYTES + LREC_LAT0;

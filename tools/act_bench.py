@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--n", type=int, default=50)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--lib", default=None)
+    ap.add_argument("--vector-step", action="store_true",
+                    help="time the whole DQN vector step: lb_dqn_step vs act + step + replay add")
     args = ap.parse_args()
     from lbk8s import _native
     if args.lib:
@@ -49,8 +51,25 @@ def main():
     exs = {eps: _native.LBDQNExploreC(eps, 0.0, eps, 12345, vpp.data_ptr(), vpp.data_ptr() + 8, flag.data_ptr())
            for eps in (0.0, 1.0)}
 
+    from lbk8s.dqn import DeviceReplayBuffer
+    rb = DeviceReplayBuffer(16 * B, B, (R, 8), obs.device, None)
+    nxt, rew = torch.empty_like(obs), torch.empty(B, device="cuda")
+    dn = torch.empty(B, dtype=torch.uint8, device="cuda")
+    es, ec = torch.zeros(B, dtype=torch.float64, device="cuda"), torch.zeros(B, dtype=torch.float64, device="cuda")
+    m8 = masks.to(torch.uint8)
+
     def launch(mode):
         st = torch.cuda.current_stream().cuda_stream
+        ex = exs[1.0 if mode.endswith("explore") else 0.0]
+        pp = rb.pos_pp.data_ptr()
+        if mode.startswith("step3"):  # the vector step as three launches: act, env step, replay write
+            env.dqn_act(frag, obs, m8, ex, act)
+            env.step_device(act, obs_out=nxt, reward_out=rew, done_out=dn)
+            rb.add_fused(obs, nxt, act, rew, dn, env.ep_stats, es, ec, 0)
+            return
+        if mode.startswith("dqn_step"):  # lb_dqn_step (one launch at config 5's shape)
+            env.dqn_step(frag, obs, m8, ex, act, nxt, rew, dn, rb, pp, pp + 8, es, ec)
+            return
         if mode == "q_argmax":
             _native.check(L.lb_ds_q_argmax(frag.data_ptr(), obs.data_ptr(), B, R, masks.data_ptr(), None,
                                            act.data_ptr(), st))
@@ -58,7 +77,9 @@ def main():
             env.dqn_act(frag, obs, masks, exs[0.0 if mode == "greedy" else 1.0], act)
 
     lib = os.path.basename(_native.LIB_PATH)
-    for mode in ("greedy", "explore", "q_argmax"):
+    modes = ("greedy", "explore", "q_argmax") if not args.vector_step else \
+        ("step3_greedy", "dqn_step_greedy", "step3_explore", "dqn_step_explore")
+    for mode in modes:
         launch(mode)
         torch.cuda.synchronize()
         side = torch.cuda.Stream()

@@ -18,7 +18,7 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 
 // one 64-env group per 64-thread block (k_rollout_lean's grid); LDSB bytes of LDS per block
 // limit the waves per CU as the real kernel's image does (10 KB: 16 per CU)
-template <int LDSB, int GROUPS>
+template <int LDSB, int GROUPS, int ROT = 0>
 __global__ __launch_bounds__(64) void k_write(float4* obs, float* rew, unsigned char* done, long B, int P, int K,
                                               long ngroups) {
     __shared__ int pad[LDSB / 4];
@@ -32,7 +32,13 @@ __global__ __launch_bounds__(64) void k_write(float4* obs, float* rew, unsigned 
             if (grp >= ngroups) break;
             const long env0 = grp * 64;
             float4* ob = obs + k * slot + env0 * P;
-            for (int it = 0; it < P; ++it) {
+            // ROT: the wave issues its P store instructions starting from a per-wave offset, so
+            // waves in lockstep write different 1-KB pieces of their blocks at the same time
+            const int r0 = ROT == 1 ? (int)(grp % P) : ROT == 2 ? (int)((grp * 7) % P) : 0;
+            for (int j = 0; j < P; ++j) {
+                int it = j + r0;
+                if (it >= P) it -= P;
+                if (ROT == 3 && (grp & 1)) it = P - 1 - j;
                 float4 v = make_float4(acc, (float)it, (float)k, 1.f);
                 __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(ob + 64 * it + lane));
             }
@@ -83,6 +89,12 @@ int main() {
         for (int K : {20, 100}) {
             run("lean grid, 10 KB LDS (4 waves/SIMD)", [&](int k) {
                 hipLaunchKernelGGL((k_write<10240, 1>), dim3((unsigned)ng), dim3(64), 0, 0, obs, rew, done, B, P, k, ng); }, K);
+            run("lean grid, 10 KB LDS, store order rotated by wave", [&](int k) {
+                hipLaunchKernelGGL((k_write<10240, 1, 1>), dim3((unsigned)ng), dim3(64), 0, 0, obs, rew, done, B, P, k, ng); }, K);
+            run("lean grid, 10 KB LDS, store order rotated by 7 x wave", [&](int k) {
+                hipLaunchKernelGGL((k_write<10240, 1, 2>), dim3((unsigned)ng), dim3(64), 0, 0, obs, rew, done, B, P, k, ng); }, K);
+            run("lean grid, 10 KB LDS, odd waves reversed", [&](int k) {
+                hipLaunchKernelGGL((k_write<10240, 1, 3>), dim3((unsigned)ng), dim3(64), 0, 0, obs, rew, done, B, P, k, ng); }, K);
             run("lean grid, 20 KB LDS (2 waves/SIMD)", [&](int k) {
                 hipLaunchKernelGGL((k_write<20480, 1>), dim3((unsigned)ng), dim3(64), 0, 0, obs, rew, done, B, P, k, ng); }, K);
             run("lean grid, 4 KB LDS (8 waves/SIMD)", [&](int k) {
