@@ -998,35 +998,31 @@ int lb_dqn_act(const float* frag, const float* obs, int64_t num_envs, int32_t nu
     return check_launch();
 }
 
-int lb_dqn_step(const float* frag, float* obs, int64_t num_envs, int32_t num_elements, const uint8_t* masks,
-                void* state, const lb_config* cfg, const lb_dqn_explore* ex, int32_t* actions_out,
-                float* next_obs_out, float* reward_out, uint8_t* done_out, float* terminal_obs_out,
-                double* ep_stats_out, int64_t slots, const int64_t* pos_in, int64_t* pos_out, float* rb_obs,
-                float* rb_next_obs, int64_t* rb_actions, float* rb_rewards, float* rb_dones, double* ep_sum,
-                double* ep_cnt, void* stream) {
-    if (int r = validate(cfg)) return r;
+namespace {
+// lb_dqn_step's one-launch shape: the env in the slice layout with 16 lanes per env (E <= 16
+// below 32,768 envs), R <= 16, at least four envs per SIMD
+bool dqn_step_fusable(const lb_config* cfg, int64_t num_envs, int32_t num_elements) {
     const Geo g = geometry(cfg, num_envs);
     const int64_t simds = (int64_t)device_cus() * 4;
-    const bool fused = !g.tpe && g.W == 16 && g.EPL == 1 && num_elements <= 16 && (num_envs + DQN_P - 1) / DQN_P >= simds;
-    if (!fused) {  // the three launches
-        if (int rc = lb_dqn_act(frag, obs, num_envs, num_elements, masks, state, cfg, ex, actions_out, stream)) return rc;
-        if (int rc = lb_step(state, cfg, num_envs, actions_out, next_obs_out, reward_out, done_out, terminal_obs_out,
-                             ep_stats_out, nullptr, stream))
-            return rc;
-        return lb_replay_add(num_envs, num_elements * 8, slots, pos_in, pos_out, obs, next_obs_out, actions_out,
-                             reward_out, done_out, ep_stats_out, rb_obs, rb_next_obs, rb_actions, rb_rewards, rb_dones,
-                             ep_sum, ep_cnt, stream);
-    }
+    return !g.tpe && g.W == 16 && g.EPL == 1 && num_elements <= 16 && (num_envs + DQN_P - 1) / DQN_P >= simds;
+}
+
+int dqn_steps_launch(const float* frag, float* obs, int64_t num_envs, int32_t num_elements, const uint8_t* masks,
+                     void* state, const lb_config* cfg, const lb_dqn_explore* ex, int32_t* actions_out,
+                     float* next_obs_out, float* reward_out, uint8_t* done_out, float* terminal_obs_out,
+                     double* ep_stats_out, int64_t slots, const int64_t* pos_in, int64_t* pos_out, float* rb_obs,
+                     float* rb_next_obs, int64_t* rb_actions, float* rb_rewards, float* rb_dones, double* ep_sum,
+                     double* ep_cnt, int32_t steps, int32_t* sync, void* stream) {
     // (the three entry points' checks)
     if (!frag || !obs || !state || !ex || !actions_out || !next_obs_out || !reward_out || !done_out || num_envs < 1)
         return fail("lb_dqn_step: frag/obs/state/ex/actions/next_obs/reward/done NULL or num_envs < 1");
-    if (!ex->vstep_in || !ex->vstep_out || ex->vstep_in == ex->vstep_out || !ex->explore_out)
+    if (!ex->vstep_in || !ex->vstep_out || (!sync && ex->vstep_in == ex->vstep_out) || !ex->explore_out)
         return fail("lb_dqn_explore: device words NULL (or vstep_in == vstep_out)");
     if (cfg->rng_mode != LB_RNG_PHILOX) return fail("lb_dqn_step draws in Philox mode only");
     const int32_t A = cfg->num_endpoints + (cfg->rejection_allowed ? 1 : 0);
     if (num_elements != A) return fail("lb_dqn_step: num_elements must be the env's action count (R)");
-    if (slots < 1 || !pos_in || !pos_out || pos_in == pos_out || !rb_obs || !rb_next_obs || !rb_actions ||
-        !rb_rewards || !rb_dones || ((ep_sum || ep_cnt) && !(ep_sum && ep_cnt && ep_stats_out)))
+    if (slots < 1 || !pos_in || !pos_out || (!sync && pos_in == pos_out) || !rb_obs || !rb_next_obs ||
+        !rb_actions || !rb_rewards || !rb_dones || ((ep_sum || ep_cnt) && !(ep_sum && ep_cnt && ep_stats_out)))
         return fail("replay buffers NULL (or pos_in == pos_out)");
     Params e = make_params(state, cfg, num_envs);
     e.obs = next_obs_out;
@@ -1047,8 +1043,51 @@ int lb_dqn_step(const float* frag, float* obs, int64_t num_envs, int32_t num_ele
                 reinterpret_cast<float4*>(rb_obs), reinterpret_cast<float4*>(rb_next_obs), rb_actions, rb_rewards,
                 rb_dones, ep_sum, ep_cnt};
     const unsigned grid = ds_grid_spread((num_envs + DQN_P - 1) / DQN_P);
-    hipLaunchKernelGGL(k_dqn_step, dim3(grid), dim3(DS_BLOCK), 0, (hipStream_t)stream, d, e, r);
+    hipLaunchKernelGGL(k_dqn_step, dim3(grid), dim3(DS_BLOCK), 0, (hipStream_t)stream, d, e, r, (int)steps, sync);
     return check_launch();
+}
+}  // namespace
+
+int lb_dqn_step(const float* frag, float* obs, int64_t num_envs, int32_t num_elements, const uint8_t* masks,
+                void* state, const lb_config* cfg, const lb_dqn_explore* ex, int32_t* actions_out,
+                float* next_obs_out, float* reward_out, uint8_t* done_out, float* terminal_obs_out,
+                double* ep_stats_out, int64_t slots, const int64_t* pos_in, int64_t* pos_out, float* rb_obs,
+                float* rb_next_obs, int64_t* rb_actions, float* rb_rewards, float* rb_dones, double* ep_sum,
+                double* ep_cnt, void* stream) {
+    if (int r = validate(cfg)) return r;
+    if (!dqn_step_fusable(cfg, num_envs, num_elements)) {  // the three launches
+        if (int rc = lb_dqn_act(frag, obs, num_envs, num_elements, masks, state, cfg, ex, actions_out, stream)) return rc;
+        if (int rc = lb_step(state, cfg, num_envs, actions_out, next_obs_out, reward_out, done_out, terminal_obs_out,
+                             ep_stats_out, nullptr, stream))
+            return rc;
+        return lb_replay_add(num_envs, num_elements * 8, slots, pos_in, pos_out, obs, next_obs_out, actions_out,
+                             reward_out, done_out, ep_stats_out, rb_obs, rb_next_obs, rb_actions, rb_rewards, rb_dones,
+                             ep_sum, ep_cnt, stream);
+    }
+    return dqn_steps_launch(frag, obs, num_envs, num_elements, masks, state, cfg, ex, actions_out, next_obs_out,
+                            reward_out, done_out, terminal_obs_out, ep_stats_out, slots, pos_in, pos_out, rb_obs,
+                            rb_next_obs, rb_actions, rb_rewards, rb_dones, ep_sum, ep_cnt, 1, nullptr, stream);
+}
+
+int lb_dqn_steps_supported(const lb_config* cfg, int64_t num_envs, int32_t num_elements) {
+    if (validate(cfg)) return 0;
+    return dqn_step_fusable(cfg, num_envs, num_elements) ? 1 : 0;
+}
+
+int lb_dqn_steps(const float* frag, float* obs, int64_t num_envs, int32_t num_elements, const uint8_t* masks,
+                 void* state, const lb_config* cfg, const lb_dqn_explore* ex, int32_t* actions_out,
+                 float* next_obs_out, float* reward_out, uint8_t* done_out, float* terminal_obs_out,
+                 double* ep_stats_out, int64_t slots, const int64_t* pos_in, int64_t* pos_out, float* rb_obs,
+                 float* rb_next_obs, int64_t* rb_actions, float* rb_rewards, float* rb_dones, double* ep_sum,
+                 double* ep_cnt, int32_t steps, int32_t* sync, void* stream) {
+    if (int r = validate(cfg)) return r;
+    if (steps < 1 || steps > 32) return fail("lb_dqn_steps: steps must be in [1, 32]");
+    if (!sync) return fail("lb_dqn_steps: sync (a device int32 that is 0) is required");
+    if (!dqn_step_fusable(cfg, num_envs, num_elements))
+        return fail("lb_dqn_steps: the env's shape has no one-launch vector step (lb_dqn_steps_supported)");
+    return dqn_steps_launch(frag, obs, num_envs, num_elements, masks, state, cfg, ex, actions_out, next_obs_out,
+                            reward_out, done_out, terminal_obs_out, ep_stats_out, slots, pos_in, pos_out, rb_obs,
+                            rb_next_obs, rb_actions, rb_rewards, rb_dones, ep_sum, ep_cnt, steps, sync, stream);
 }
 
 int lb_dqn_head(const float* q, const float* q_next, const int64_t* actions, const float* rewards, const float* dones,

@@ -38,18 +38,31 @@ struct DQNReplay {  // lb_replay_add's buffers
 // d: the Q forward (lb_dqn_act's DSParams: obs, the actor-only weight image, masks, actions,
 // the explore struct); e: the env (lb_step's Params: obs = the next observations, reward,
 // done, terminal obs, ep_stats); r: the replay buffer.
-__global__ __launch_bounds__(DS_BLOCK, 2) void k_dqn_step(DSParams d, Params e, DQNReplay r) {
+//
+// nsteps > 1 (lb_dqn_steps): that many vector steps in the one launch.  Within a DQN train
+// period the Q network is fixed (the train step follows the period's last vector step) and
+// every env's chain touches no other env, so each wave takes its four envs through all the
+// steps: step i explores by dqn_explores(t + i) (the same draw for every env), writes replay
+// slot pos + i, and leaves obs <- next obs and the env state for step i + 1, which the same
+// wave reads back after an s_waitcnt vmcnt(0).  The device words (vstep, pos, explore flag)
+// are then written by the launch's last block (sync: a counter the launch leaves at 0), after
+// every block has read them: in and out may be the same words.
+__global__ __launch_bounds__(DS_BLOCK, 2) void k_dqn_step(DSParams d, Params e, DQNReplay r, int nsteps,
+                                                         int32_t* sync) {
     constexpr int P = DQN_P, NWB = DS_BLOCK / 64;
     const int64_t t = *d.ex.vstep_in;
     const int64_t pos = *r.pos_in;
-    const bool explore = dqn_explores(d.ex, t);  // (:127, uniform over the launch)
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        *d.ex.explore_out = explore ? 1 : 0;
+    uint32_t exm = 0;  // step i explores: bit i (:127, uniform over the launch)
+    for (int i = 0; i < nsteps; ++i)
+        if (dqn_explores(d.ex, t + i)) exm |= 1u << i;
+    if (!sync && blockIdx.x == 0 && threadIdx.x == 0) {  // (nsteps == 1: in and out differ)
+        *d.ex.explore_out = (int32_t)(exm & 1u);
         *d.ex.vstep_out = t + 1;
         *r.pos_out = (pos + 1) % r.slots;
     }
     __shared__ __attribute__((aligned(16))) float W[DS_C1L];  // the Q network's fragments
-    if (!explore) {
+    const uint32_t all = nsteps >= 32 ? ~0u : (1u << nsteps) - 1u;
+    if (exm != all) {  // (some step is greedy)
         for (int i = threadIdx.x * 4; i < DS_C1L; i += DS_BLOCK * 4)
             *reinterpret_cast<float4*>(W + i) = *reinterpret_cast<const float4*>(d.wfrag + i);
         __syncthreads();
@@ -63,44 +76,65 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_dqn_step(DSParams d, Params e, 
     const int s = lane >> 4, l16 = lane & 15;
     for (int64_t gi = wave; gi < groups; gi += nwaves) {
         const int64_t env0 = gi * P;
-        // the greedy actions of the group's envs (lane s holds env0 + s's; :134-142)
-        int32_t act = -1;
-        if (!explore) {
-            float h0[P][2], m0[2];
-            ds_group_obs<1, P, 2>(d, env0, col, grp, R, h0, m0);
-            act = ds_group_actor<1, P, 2>(d, W, lane, env0, col, grp, R, h0, m0);
-        }
-        const int32_t ag = __shfl(act, s);
-        // the env step: lanes 16 s .. 16 s + 15 step env env0 + s (k_step_slice<16, 1>'s body)
-        const int64_t env = env0 + s;
-        int a = 0;
-        if (env < e.B) {
-            SEnv<1> v;
-            slice_load<16, 1>(e, env, l16, v);
-            a = explore ? random_action(e, env, v.acc3, v.s.step) : ag;  // (exploring: :128-131)
-            if (explore && l16 == 0) d.actions[env] = a;
-            slice_step_body<16, 1, false, true, NWB>(e, env, l16, v, a, e.obs, e.reward, e.done, e.rew64);
-            if (l16 == 0) slice_store_scalars<1>(e, env, v);
-        }
-        // the group's replay rows (lb_replay_add's), once the step's outputs have landed
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int64_t hi = (env0 + P < e.B ? env0 + P : e.B) * r.f4;
-        const float4* nxo = reinterpret_cast<const float4*>(e.obs);
-        for (int64_t i = env0 * r.f4 + lane; i < hi; i += 64) {
-            const float4 o = r.obs[i], nx = nxo[i];
-            r.rb_obs[pos * n4 + i] = o;
-            r.rb_next_obs[pos * n4 + i] = nx;
-            r.obs[i] = nx;
-        }
-        if (l16 == 0 && env < e.B) {  // (the lane that wrote the env's reward, done and stats row)
-            const bool dn = e.done[env] != 0;
-            r.rb_actions[pos * e.B + env] = a;
-            r.rb_rewards[pos * e.B + env] = e.reward[env];
-            r.rb_dones[pos * e.B + env] = dn ? 1.f : 0.f;
-            if (r.ep_sum && dn) {
-                r.ep_sum[env] += e.ep_stats[env * LB_ST_K];
-                r.ep_cnt[env] += 1.0;
+        for (int i = 0; i < nsteps; ++i) {
+            const bool explore = (exm >> i) & 1u;
+            const int64_t ps = (pos + i) % r.slots;
+            // the greedy actions of the group's envs (lane s holds env0 + s's; :134-142)
+            int32_t act = -1;
+            if (!explore) {
+                float h0[P][2], m0[2];
+                ds_group_obs<1, P, 2>(d, env0, col, grp, R, h0, m0);
+                act = ds_group_actor<1, P, 2>(d, W, lane, env0, col, grp, R, h0, m0);
             }
+            const int32_t ag = __shfl(act, s);
+            // the env step: lanes 16 s .. 16 s + 15 step env env0 + s (k_step_slice<16, 1>'s body)
+            const int64_t env = env0 + s;
+            int a = 0;
+            if (env < e.B) {
+                SEnv<1> v;
+                slice_load<16, 1>(e, env, l16, v);
+                a = explore ? random_action(e, env, v.acc3, v.s.step) : ag;  // (exploring: :128-131)
+                if (explore && l16 == 0) d.actions[env] = a;
+                slice_step_body<16, 1, false, true, NWB>(e, env, l16, v, a, e.obs, e.reward, e.done, e.rew64);
+                if (l16 == 0) slice_store_scalars<1>(e, env, v);
+            }
+            // the group's replay rows (lb_replay_add's), once the step's outputs have landed
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int64_t hi = (env0 + P < e.B ? env0 + P : e.B) * r.f4;
+            const float4* nxo = reinterpret_cast<const float4*>(e.obs);
+            for (int64_t j = env0 * r.f4 + lane; j < hi; j += 64) {
+                const float4 o = r.obs[j], nx = nxo[j];
+                r.rb_obs[ps * n4 + j] = o;
+                r.rb_next_obs[ps * n4 + j] = nx;
+                r.obs[j] = nx;
+            }
+            if (l16 == 0 && env < e.B) {  // (the lane that wrote the env's reward, done and stats row)
+                const bool dn = e.done[env] != 0;
+                r.rb_actions[ps * e.B + env] = a;
+                r.rb_rewards[ps * e.B + env] = e.reward[env];
+                r.rb_dones[ps * e.B + env] = dn ? 1.f : 0.f;
+                if (r.ep_sum && dn) {
+                    r.ep_sum[env] += e.ep_stats[env * LB_ST_K];
+                    r.ep_cnt[env] += 1.0;
+                }
+            }
+            // (step i + 1 reads the obs, the env state and the sums back)
+            if (i + 1 < nsteps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    if (sync) {  // the last block to finish writes the device words (every block has read them)
+        __shared__ int last;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            last = atomicAdd(sync, 1) == (int)gridDim.x - 1;
+        }
+        __syncthreads();
+        if (last && threadIdx.x == 0) {
+            *d.ex.explore_out = (int32_t)((exm >> (nsteps - 1)) & 1u);
+            *d.ex.vstep_out = t + nsteps;
+            *r.pos_out = (pos + nsteps) % r.slots;
+            *sync = 0;
         }
     }
 }

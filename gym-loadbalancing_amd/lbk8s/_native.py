@@ -15,7 +15,7 @@ CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
 # csrc/Makefile's SRCS, in order: the library embeds the SHA-256 of their concatenation
 SOURCES = ("lbk8s.hip", "lbk8s_common.h", "lbk8s_slice.h", "lbk8s_tpe.h", "lbk8s_rollout.h", "lbk8s_lean.h",
            "lbk8s_deepsets.h", "lbk8s_ds_train.h", "lbk8s_dqn.h", "../../include/lbk8s.h")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 LB_REWARD = {"naive": 0, "latency": 1, "fairness": 2, "multi": 3}
 LB_RNG_PHILOX, LB_RNG_TRACE = 0, 1
@@ -177,6 +177,8 @@ def lib():
     L.lb_dqn_act.argtypes = [vp, vp, i64, i32, vp, vp, cfgp, C.POINTER(LBDQNExploreC), vp, vp]
     L.lb_dqn_step.argtypes = [vp, vp, i64, i32, vp, vp, cfgp, C.POINTER(LBDQNExploreC), vp, vp, vp, vp, vp, vp,
                               i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.lb_dqn_steps.argtypes = L.lb_dqn_step.argtypes[:-1] + [i32, vp, vp]
+    L.lb_dqn_steps_supported.argtypes = [cfgp, i64, i32]
     L.lb_dqn_head.argtypes = [vp, vp, vp, vp, vp, i64, i32, C.c_float, vp, vp, vp, vp, vp]
     L.lb_replay_sample.argtypes = [i64, i32, i64, i32, C.c_uint64] + [vp] * 12 + [vp]
     L.lb_ds_set_grads.argtypes = [vp, vp, vp, i64, i32, vp, vp]
@@ -185,7 +187,8 @@ def lib():
               "lb_get_field", "lb_get_stats", "lb_status", "lb_ds_pack", "lb_ds_forward",
               "lb_ds_train_forward", "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax",
               "lb_replay_add", "lb_ppo_head", "lb_episode_log", "lb_dqn_act", "lb_dqn_head",
-              "lb_replay_sample", "lb_ds_set_grads", "lb_dqn_step"):
+              "lb_replay_sample", "lb_ds_set_grads", "lb_dqn_step", "lb_dqn_steps",
+              "lb_dqn_steps_supported"):
         getattr(L, f).restype = C.c_int
     v = L.lb_abi_version()
     if v != ABI_VERSION and product:
@@ -215,4 +218,5 @@ EXPORTED_SYMBOLS = ("lb_abi_version", "lb_last_error", "lb_validate_config", "lb
                     "lb_status", "lb_ds_pack", "lb_ds_forward", "lb_ds_train_forward",
                     "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax", "lb_replay_add", "lb_ppo_head",
                     "lb_episode_log", "lb_dqn_act", "lb_dqn_head", "lb_replay_sample", "lb_ds_set_grads",
-                    "lb_rollout_kernel", "lb_source_hash", "lb_reward64", "lb_dqn_step")
+                    "lb_rollout_kernel", "lb_source_hash", "lb_reward64", "lb_dqn_step",
+                    "lb_dqn_steps", "lb_dqn_steps_supported")

@@ -140,7 +140,7 @@ class DQN_DeepSets:
                  buffer_size=10000, gamma=0.99, tau=1.0, n_minibatches: int = 4, target_network_frequency=500,
                  batch_size=128, start_e=1, end_e=0.05, exploration_fraction=0.5, learning_starts=10000,
                  train_frequency=10, device=None, log_fn=None, num_envs=None, tensorboard_log=None,
-                 train_graph=None, period_graph=None, device_rng=None):
+                 train_graph=None, period_graph=None, device_rng=None, multi_step=None):
         # num_envs / tensorboard_log: accepted for signature compatibility with
         # dqn_deepset.py:46-67 (the env's num_envs is used; there is no tensorboard writer)
         self.env = env
@@ -205,6 +205,10 @@ class DQN_DeepSets:
         self._explore_flag = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._base_adds = torch.zeros(1, dtype=torch.int64, device=self.device)
         self._ex = [None, None]  # LBDQNExploreC per parity (kept alive: graphs hold their pointers' targets)
+        self._ex_same = [None, None]
+        # a train period's vector steps in one launch where the env allows it (lb_dqn_steps)
+        self.multi_step = (os.environ.get("LBK8S_DQN_MULTISTEP", "1") == "1") if multi_step is None else bool(multi_step)
+        self._dqn_sync = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._pgraphs = {}
         self._pgraph_slope = None
         self._tstatic = None
@@ -258,6 +262,9 @@ class DQN_DeepSets:
         for parity in (0, 1):
             self._ex[parity] = LBDQNExploreC(self.start_e, slope, self.end_e, self._rng_seed, base + 8 * parity,
                                              base + 8 * (1 - parity), self._explore_flag.data_ptr())
+            # (lb_dqn_steps over an even number of steps: the counter ends in the word it started in)
+            self._ex_same[parity] = LBDQNExploreC(self.start_e, slope, self.end_e, self._rng_seed, base + 8 * parity,
+                                                  base + 8 * parity, self._explore_flag.data_ptr())
         return slope
 
     def _vector_step_dev(self, obs, masks, parity):
@@ -268,6 +275,19 @@ class DQN_DeepSets:
         # (lb_dqn_step: the three in one launch at config 5's shape, bit for bit)
         env.dqn_step(self._qfrag, obs, masks, self._ex[parity], self._act, self._next_obs, self._rew, self._done_u8,
                      self.rb, pp + 8 * parity, pp + 8 * (1 - parity), self._ep_sum, self._ep_cnt)
+
+    def _vector_steps_dev(self, obs, masks, parity, n):
+        """n vector steps from `parity`: one lb_dqn_steps launch where the env's shape has the
+        one-launch step (the Q network is fixed within a period), else n _vector_step_dev."""
+        env, pp = self.env, self.rb.pos_pp.data_ptr()
+        if n > 1 and self.multi_step and env.dqn_steps_supported(obs.shape[1]):
+            end = parity ^ (n & 1)
+            ex = self._ex[parity] if end != parity else self._ex_same[parity]
+            env.dqn_steps(n, self._qfrag, obs, masks, ex, self._act, self._next_obs, self._rew, self._done_u8,
+                          self.rb, pp + 8 * parity, pp + 8 * end, self._ep_sum, self._ep_cnt, self._dqn_sync)
+            return
+        for i in range(n):
+            self._vector_step_dev(obs, masks, parity ^ (i & 1))
 
     def _sample_dev(self, parity):
         """lb_replay_sample into the train step's fixed buffers; the counter is the vector step
@@ -287,8 +307,7 @@ class DQN_DeepSets:
         """n vector steps from `parity` then (train) the sample and the train step; returns
         the graphs' split point for the all_reduce (multi-rank) via self._period_split."""
         fused.pack_q_into(self.q_network, self._qfrag)
-        for i in range(n):
-            self._vector_step_dev(obs, masks, parity ^ (i & 1))
+        self._vector_steps_dev(obs, masks, parity, n)
         if train:
             self._sample_dev(parity ^ (n & 1))
             self._tloss = self._train_backward(*self._tstatic)

@@ -500,6 +500,25 @@ class LBVecEnv:
             self._ptr(ep_sum), self._ptr(ep_cnt), self._stream()))
         return actions
 
+    def dqn_steps_supported(self, R):
+        """Whether lb_dqn_steps (several DQN vector steps in one launch) covers this env with
+        R-row observations."""
+        return bool(self._L.lb_dqn_steps_supported(C.byref(self._c), self.num_envs, R))
+
+    def dqn_steps(self, n, frag, obs, masks, ex, actions, next_obs, reward, done, rb, pos_in, pos_out, ep_sum, ep_cnt,
+                  sync):
+        """lb_dqn_steps: n DQN vector steps (dqn_step n times, the explore draw, replay slot and
+        step counter advancing per step) in one launch; pos_in / pos_out and the explore
+        struct's step words may coincide.  sync: a device int32 tensor holding 0."""
+        R = obs.shape[1]
+        _native.check(self._L.lb_dqn_steps(
+            frag.data_ptr(), obs.data_ptr(), self.num_envs, R, self._ptr(masks), self._ptr(self.state),
+            C.byref(self._c), C.byref(ex), self._ptr(actions), self._ptr(next_obs), self._ptr(reward), self._ptr(done),
+            self._ptr(self.terminal_obs), self._ptr(self.ep_stats), rb.size, pos_in, pos_out, rb.obs.data_ptr(),
+            rb.next_obs.data_ptr(), rb.actions.data_ptr(), rb.rewards.data_ptr(), rb.dones.data_ptr(),
+            self._ptr(ep_sum), self._ptr(ep_cnt), int(n), sync.data_ptr(), self._stream()))
+        return actions
+
     def field(self, name):
         """Env attribute as a float64 device tensor: (B, E) or (B,)."""
         shape = (self.num_envs,) if name in _native.PER_ENV_FIELDS else (self.num_envs, self.cfg.num_endpoints)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LBK8S_ABI_VERSION 9
+#define LBK8S_ABI_VERSION 10
 
 /* reward_function names of loadbalancer_k8s_env.py:20-31 */
 enum { LB_REWARD_NAIVE = 0, LB_REWARD_LATENCY = 1, LB_REWARD_FAIRNESS = 2, LB_REWARD_MULTI = 3 };
@@ -307,6 +307,23 @@ int lb_dqn_step(const float* frag, float* obs, int64_t num_envs, int32_t num_ele
                 double* ep_stats_out, int64_t slots, const int64_t* pos_in, int64_t* pos_out, float* rb_obs,
                 float* rb_next_obs, int64_t* rb_actions, float* rb_rewards, float* rb_dones, double* ep_sum,
                 double* ep_cnt, void* stream);
+
+/* `steps` DQN vector steps (1..32) in ONE launch (ABI 10): lb_dqn_step `steps` times with the
+ * explore draw, the replay slot and the step counter advancing per step, bit for bit, where
+ * lb_dqn_steps_supported(cfg, num_envs, num_elements) is 1 (lb_dqn_step's one-launch shape;
+ * else it fails).  Within a DQN train period (envs/dqn_deepset.py:122-174 between two train
+ * steps, :176-205) the Q network is fixed and each env's chain touches no other env.  Reads
+ * *ex->vstep_in / *pos_in, writes the step counter + steps / (pos + steps) % slots / the last
+ * step's explore flag to *ex->vstep_out / *pos_out / *ex->explore_out, which may be the same
+ * words as the inputs: they are written by the launch's last block.  sync: a device int32
+ * that is 0 (the launch leaves it at 0). */
+int lb_dqn_steps_supported(const lb_config* cfg, int64_t num_envs, int32_t num_elements);
+int lb_dqn_steps(const float* frag, float* obs, int64_t num_envs, int32_t num_elements, const uint8_t* masks,
+                 void* state, const lb_config* cfg, const lb_dqn_explore* ex, int32_t* actions_out,
+                 float* next_obs_out, float* reward_out, uint8_t* done_out, float* terminal_obs_out,
+                 double* ep_stats_out, int64_t slots, const int64_t* pos_in, int64_t* pos_out, float* rb_obs,
+                 float* rb_next_obs, int64_t* rb_actions, float* rb_rewards, float* rb_dones, double* ep_sum,
+                 double* ep_cnt, int32_t steps, int32_t* sync, void* stream);
 
 /* DQN loss head (dqn_deepset.py:180-187): per sample td = r + gamma max q_next (1 - done),
  * sq_err_out = (td - q[a])^2 (mean = F.mse_loss) and dq_out = d mean / d q (2 (q[a] - td) /

@@ -71,3 +71,44 @@ def test_dqn_step_equals_three_launches(B, kw):
         assert torch.equal(a_env.field(f), b_env.field(f)), f
     assert explored > 0 and greedy > 0
     assert int(a["ep_cnt"].sum().item()) > 0  # episodes ended inside the window
+
+
+@pytest.mark.parametrize("B,kw,n", [(4096, {}, 10), (4096 + 8, dict(reward_function="multi", episode_length=9), 7),
+                                    (8192, dict(num_endpoints=6, reward_function="fairness"), 2)])
+def test_dqn_steps_equals_single_steps(B, kw, n):
+    """lb_dqn_steps(n) (n vector steps in one launch, the device words in place for even n)
+    == n x lb_dqn_step with the ping-pong words, bit for bit, over launches that cross the
+    explore / greedy boundary and episode ends."""
+    kw = dict(dict(episode_length=7), **kw)
+    a_env, frag, a_rb, a, nat = _setup(B, kw, seed=9)
+    b_env, _, b_rb, b, _ = _setup(B, kw, seed=9)
+    assert a_env.dqn_steps_supported(a_env.cfg.obs_rows)
+    masks = torch.ones((B, a_env.cfg.obs_rows), dtype=torch.uint8, device="cuda")
+    sync = torch.zeros(1, dtype=torch.int32, device="cuda")
+    pa, pb = a_rb.pos_pp.data_ptr(), b_rb.pos_pp.data_ptr()
+    va = a["vpp"].data_ptr()
+    parity = 0
+    flags = set()
+    for _ in range(48 // n):
+        end = parity ^ (n & 1)
+        ex_a = nat.LBDQNExploreC(0.9, -(0.9 - 0.05) / 40.0, 0.05, 77, va + 8 * parity, va + 8 * end, a["flag"].data_ptr())
+        a_env.dqn_steps(n, frag, a["obs"], masks, ex_a, a["act"], a["next_obs"], a["rew"], a["done"], a_rb,
+                        pa + 8 * parity, pa + 8 * end, a["ep_sum"], a["ep_cnt"], sync)
+        for i in range(n):
+            q = parity ^ (i & 1)
+            b_env.dqn_step(frag, b["obs"], masks, _ex(nat, b, q, 0.9), b["act"], b["next_obs"], b["rew"], b["done"],
+                           b_rb, pb + 8 * q, pb + 8 * (1 - q), b["ep_sum"], b["ep_cnt"])
+        parity = end
+        flags.add(int(b["flag"].item()))
+        assert int(a["flag"].item()) == int(b["flag"].item())
+        assert int(sync.item()) == 0
+        assert int(a["vpp"][parity].item()) == int(b["vpp"][parity].item())
+        assert int(a_rb.pos_pp[parity].item()) == int(b_rb.pos_pp[parity].item())
+        for k in ("act", "next_obs", "rew", "done", "obs", "ep_sum", "ep_cnt"):
+            assert torch.equal(a[k], b[k]), k
+        assert torch.equal(a_env.terminal_obs, b_env.terminal_obs)
+        assert torch.equal(a_env.ep_stats, b_env.ep_stats)
+    for name in ("obs", "next_obs", "actions", "rewards", "dones"):
+        assert torch.equal(getattr(a_rb, name), getattr(b_rb, name)), name
+    assert torch.equal(a_env.stats(), b_env.stats())
+    assert int(a["ep_cnt"].sum().item()) > 0

@@ -68,6 +68,30 @@ def test_dqn_graph_train_step_matches_eager():
         torch.testing.assert_close(b, a, rtol=1e-4, atol=2e-6)
 
 
+def test_dqn_multi_step_periods_match_single_steps():
+    """At config 5's shape (4096 envs: the one-launch vector step) a train period's vector steps
+    run as ONE lb_dqn_steps launch; the learner then follows exactly the trajectory of one
+    lb_dqn_step launch per vector step: same replay contents, parameters, env state and
+    episode sums (period graphs on both sides; 10-step periods, even, so the device words
+    are updated in place, and the 1-step periods around them)."""
+    from lbk8s import LBVecEnv
+    from lbk8s.dqn import DQN_DeepSets
+    res = []
+    for multi in (False, True):
+        env = LBVecEnv(4096, seed=4, as_tensors=True, episode_length=10)
+        algo = DQN_DeepSets(env, buffer_size=4096 * 40, batch_size=128, learning_starts=15, train_frequency=10,
+                            target_network_frequency=40, seed=1, multi_step=multi)
+        assert algo.period_graph and env.dqn_steps_supported(env.cfg.obs_rows)
+        algo.learn(total_timesteps=62)
+        res.append(([p.detach().clone() for p in algo.q_network.parameters()], algo.rb.obs.clone(),
+                     algo.rb.actions.clone(), env.stats(), list(algo.episode_returns), algo.rb.pos_pp.clone()))
+    (pa, oa, aa, sa, ea, qa), (pb, ob, ab, sb, eb, qb) = res
+    for x, y in zip(pa, pb):
+        assert torch.equal(x, y)
+    assert torch.equal(oa, ob) and torch.equal(aa, ab) and torch.equal(sa, sb) and torch.equal(qa, qb)
+    assert ea == eb and ea
+
+
 def test_ppo_graph_update_matches_eager():
     """The HIP-graph minibatch step (captured once, replayed) computes the eager update:
     two updates, so the second rollout must see the first update's weights (the fused
