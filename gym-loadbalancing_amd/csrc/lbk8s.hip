@@ -1042,8 +1042,12 @@ int dqn_steps_launch(const float* frag, float* obs, int64_t num_envs, int32_t nu
     DQNReplay r{slots, num_elements * 2, pos_in, pos_out, reinterpret_cast<float4*>(obs),
                 reinterpret_cast<float4*>(rb_obs), reinterpret_cast<float4*>(rb_next_obs), rb_actions, rb_rewards,
                 rb_dones, ep_sum, ep_cnt};
-    const unsigned grid = ds_grid_spread((num_envs + DQN_P - 1) / DQN_P);
-    hipLaunchKernelGGL(k_dqn_step, dim3(grid), dim3(DS_BLOCK), 0, (hipStream_t)stream, d, e, r, (int)steps, sync);
+#ifndef LB_DQN_P
+#define LB_DQN_P 2  // envs per wave iteration: 2 puts the 4096-env batch on every wave of the grid (4: half the waves idle)
+#endif
+    constexpr int P = LB_DQN_P;
+    const unsigned grid = ds_grid_spread((num_envs + P - 1) / P);
+    hipLaunchKernelGGL(k_dqn_step<P>, dim3(grid), dim3(DS_BLOCK), 0, (hipStream_t)stream, d, e, r, (int)steps, sync);
     return check_launch();
 }
 }  // namespace
@@ -1092,12 +1096,18 @@ int lb_dqn_steps(const float* frag, float* obs, int64_t num_envs, int32_t num_el
 
 int lb_dqn_head(const float* q, const float* q_next, const int64_t* actions, const float* rewards, const float* dones,
                 int64_t num_sets, int32_t num_elements, float gamma, float* dq_out, float* sq_err_out, float* td_out,
-                float* old_out, void* stream) {
+                float* old_out, float* loss_out, void* stream) {
     if (!q || !q_next || !actions || !rewards || !dones || !dq_out || !sq_err_out || num_sets < 1)
         return fail("lb_dqn_head: NULL buffer or num_sets < 1");
     if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS_TRAIN) return fail("num_elements must be in [1, 257]");
+    if (loss_out && num_sets > DQN_HEAD_BLOCK_MAX) return fail("lb_dqn_head: loss_out needs num_sets <= 1024");
     DQNHeadParams p{q, q_next, actions, rewards, dones, num_sets, num_elements, gamma, 2.0f / (float)num_sets, dq_out,
-                    sq_err_out, td_out, old_out};
+                    sq_err_out, td_out, old_out, loss_out};
+    if (loss_out) {  // one block, one lane per sample, the mean in the same launch
+        hipLaunchKernelGGL(k_dqn_head_block, dim3(1), dim3((unsigned)((num_sets + 63) / 64 * 64)), 0,
+                           (hipStream_t)stream, p);
+        return check_launch();
+    }
     const unsigned grid = (unsigned)std::min<int64_t>((num_sets + 3) / 4, 65535);
     hipLaunchKernelGGL(k_dqn_head, dim3(grid), dim3(256), 0, (hipStream_t)stream, p);
     return check_launch();
@@ -1137,6 +1147,30 @@ int lb_ds_train_forward(const float* frag, const float* obs, int64_t num_envs, i
     return check_launch();
 }
 
+int lb_ds_forward_pair(const float* frag_a, const float* obs_a, float* logits_a, const float* frag_b,
+                       const float* obs_b, float* logits_b, float* save_actor_b, float* setvec_b, int64_t num_envs,
+                       int32_t num_elements, void* stream) {
+    if (!frag_a || !obs_a || !logits_a || !frag_b || !obs_b || !logits_b || !save_actor_b || !setvec_b || num_envs < 1)
+        return fail("lb_ds_forward_pair: NULL buffer or num_envs < 1");
+    if (num_elements < 1 || num_elements > 16) return fail("lb_ds_forward_pair: num_elements must be in [1, 16]");
+    DSParams a{obs_a, frag_a, logits_a, nullptr, num_envs, num_elements, 1, 0,
+               nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    DSParams b{obs_b, frag_b, logits_b, nullptr, num_envs, num_elements, 1, 0,
+               save_actor_b, nullptr, nullptr, setvec_b, nullptr, nullptr};
+    // P as ds_forward_launch picks it for one of the two (the batch against the chip's SIMDs)
+    int P = 4;
+    {
+        const int64_t simds = (int64_t)device_cus() * 4 * LB_DS_WAVES_PER_SIMD;
+        while (P > 1 && (num_envs + P - 1) / P < simds) P /= 2;
+    }
+    const int ga = (int)ds_grid_spread((num_envs + P - 1) / P);
+    const dim3 grid(2 * ga);
+    if (P == 4) hipLaunchKernelGGL((k_ds_fwd_pair<1, 4>), grid, dim3(DS_BLOCK), 0, (hipStream_t)stream, a, b, ga);
+    else if (P == 2) hipLaunchKernelGGL((k_ds_fwd_pair<1, 2>), grid, dim3(DS_BLOCK), 0, (hipStream_t)stream, a, b, ga);
+    else hipLaunchKernelGGL((k_ds_fwd_pair<1, 1>), grid, dim3(DS_BLOCK), 0, (hipStream_t)stream, a, b, ga);
+    return check_launch();
+}
+
 int lb_ppo_head(const float* logits, const uint8_t* masks, const float* actions, const float* oldlogp,
                 const float* adv, const float* ret, const float* vold, const float* value, int64_t num_sets,
                 int32_t num_elements, float clip_coef, float ent_coef, float vf_coef, int32_t clip_vloss,
@@ -1159,6 +1193,15 @@ int lb_ds_pack_backward(const lb_ds_weights* w, float* bwd_frag_out, void* strea
         return fail("actor weights are required");
     hipLaunchKernelGGL(k_ds_pack_bwd, dim3((DSB_FLOATS + 255) / 256), dim3(256), 0, (hipStream_t)stream, *w,
                        bwd_frag_out);
+    return check_launch();
+}
+
+int lb_ds_pack_pair(const lb_ds_weights* w, float* frag_out, float* bwd_frag_out, void* stream) {
+    if (!w || !frag_out || !bwd_frag_out) return fail("weights/frag_out/bwd_frag_out NULL");
+    for (int i = 0; i < 3; ++i)
+        if (!w->actor_lambda[i] || !w->actor_gamma[i]) return fail("actor weights are required");
+    hipLaunchKernelGGL(k_ds_pack_pair, dim3(DS_PACK_BLOCKS + DSB_PACK_BLOCKS), dim3(256), 0, (hipStream_t)stream, *w,
+                       frag_out, bwd_frag_out);
     return check_launch();
 }
 

@@ -428,11 +428,11 @@ __device__ __forceinline__ int32_t ds_group_actor(const DSParams& p, const float
 
 // MODE 0: logits / value; 1: training forward (TRAIN: activations, psi mean); 2: Q values
 // and the masked greedy action (ARGMAX; actor only)
+// the forward of the blocks blk = 0 .. nblk - 1 (k_deepsets_fwd: the whole grid; k_ds_fwd_pair:
+// its half of the grid), W the block's LDS weight region
 template <int TS, int P, int MODE>
-__global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
+__device__ __forceinline__ void ds_fwd_body(const DSParams& p, float* W, int blk, int nblk) {
     constexpr bool TRAIN = MODE == 1, ARGMAX = MODE == 2;
-    if (ARGMAX && p.ex_on && ds_dqn_explore(p)) return;  // (uniform: the DQN step explores)
-    __shared__ __attribute__((aligned(16))) float W[DS_LDS_FLOATS];
     // stage the weight fragments (once per block; blocks are persistent); an actor-only
     // launch (DQN) stages only the actor's
     const int nstage = (ARGMAX || !p.critic) ? DS_C1L : DS_FLOATS;
@@ -442,8 +442,8 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
     const int lane = threadIdx.x & 63;
     // wave-major numbering: a batch of fewer groups than waves puts one wave on each SIMD
     // of every CU (waves 0-3 of a block sit on its 4 SIMDs) before any SIMD takes a second
-    const int64_t wave = (int64_t)(threadIdx.x >> 6) * gridDim.x + blockIdx.x;
-    const int64_t nwaves = (int64_t)gridDim.x * (DS_BLOCK / 64);
+    const int64_t wave = (int64_t)(threadIdx.x >> 6) * nblk + blk;
+    const int64_t nwaves = (int64_t)nblk * (DS_BLOCK / 64);
     const int R = p.R;
     const int col = lane & 15, grp = lane >> 4;
     const int64_t groups = (p.B + P - 1) / P;
@@ -540,6 +540,23 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
         // row 0 of the result: column c = env (c mod P)
         if (grp == 0 && col < P && env0 + col < p.B) p.value[env0 + col] = v[0];
     }
+}
+
+template <int TS, int P, int MODE>
+__global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
+    if (MODE == 2 && p.ex_on && ds_dqn_explore(p)) return;  // (uniform: the DQN step explores)
+    __shared__ __attribute__((aligned(16))) float W[DS_LDS_FLOATS];
+    ds_fwd_body<TS, P, MODE>(p, W, blockIdx.x, gridDim.x);
+}
+
+// two forwards in one launch (lb_ds_forward_pair: the DQN train step's target-network Q values
+// of the next observations and the trained network's training forward): blocks below ga run
+// a's inference forward (MODE 0), the rest b's training forward (MODE 1); actor only
+template <int TS, int P>
+__global__ __launch_bounds__(DS_BLOCK, 2) void k_ds_fwd_pair(DSParams a, DSParams b, int ga) {
+    __shared__ __attribute__((aligned(16))) float W[DS_C1L];
+    if ((int)blockIdx.x < ga) ds_fwd_body<TS, P, 0>(a, W, blockIdx.x, ga);
+    else ds_fwd_body<TS, P, 1>(b, W, blockIdx.x - ga, gridDim.x - ga);
 }
 
 // ---- large sets (LB_DS_MAX_ELEMENTS < R <= LB_DS_MAX_ELEMENTS_FWD) ------------------------
@@ -831,8 +848,7 @@ __device__ __forceinline__ float ds_frag_value(const float* w, int nout, int kin
     return (w && row < nout) ? w[row * kin + in] : 0.f;
 }
 
-__global__ void k_ds_pack(lb_ds_weights w, float* out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void ds_pack_one(const lb_ds_weights& w, float* out, int i) {
     if (i >= DS_FLOATS) return;
     // regions in layout order: (start, pointer, out features, in features, k-steps)
     const int starts[16] = {DS_A1L, DS_A1G, DS_A2L, DS_A2G, DS_A3L, DS_A3G, DS_C1L, DS_C1G,
@@ -863,5 +879,6 @@ __global__ void k_ds_pack(lb_ds_weights w, float* out) {
     const bool gamma = r == 1 || r == 3 || r == 5 || r == 7 || r == 9 || r == 11;
     out[i] = gamma ? -v : v;
 }
+__global__ void k_ds_pack(lb_ds_weights w, float* out) { ds_pack_one(w, out, blockIdx.x * blockDim.x + threadIdx.x); }
 
 }  // namespace lbk

@@ -47,9 +47,11 @@ struct DQNReplay {  // lb_replay_add's buffers
 // wave reads back after an s_waitcnt vmcnt(0).  The device words (vstep, pos, explore flag)
 // are then written by the launch's last block (sync: a counter the launch leaves at 0), after
 // every block has read them: in and out may be the same words.
+template <int P>
 __global__ __launch_bounds__(DS_BLOCK, 2) void k_dqn_step(DSParams d, Params e, DQNReplay r, int nsteps,
                                                          int32_t* sync) {
-    constexpr int P = DQN_P, NWB = DS_BLOCK / 64;
+    static_assert(P == 2 || P == 4, "envs per wave iteration");
+    constexpr int NWB = DS_BLOCK / 64;
     const int64_t t = *d.ex.vstep_in;
     const int64_t pos = *r.pos_in;
     uint32_t exm = 0;  // step i explores: bit i (:127, uniform over the launch)
@@ -86,16 +88,17 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_dqn_step(DSParams d, Params e, 
                 ds_group_obs<1, P, 2>(d, env0, col, grp, R, h0, m0);
                 act = ds_group_actor<1, P, 2>(d, W, lane, env0, col, grp, R, h0, m0);
             }
-            const int32_t ag = __shfl(act, s);
+            const int32_t ag = __shfl(act, s < P ? s : 0);
             // the env step: lanes 16 s .. 16 s + 15 step env env0 + s (k_step_slice<16, 1>'s body)
             const int64_t env = env0 + s;
             int a = 0;
-            if (env < e.B) {
+            if (s < P && env < e.B) {
                 SEnv<1> v;
                 slice_load<16, 1>(e, env, l16, v);
                 a = explore ? random_action(e, env, v.acc3, v.s.step) : ag;  // (exploring: :128-131)
                 if (explore && l16 == 0) d.actions[env] = a;
-                slice_step_body<16, 1, false, true, NWB>(e, env, l16, v, a, e.obs, e.reward, e.done, e.rew64);
+                slice_step_body<16, 1, false, true, P == 4 ? NWB : 0>(e, env, l16, v, a, e.obs, e.reward, e.done,
+                                                                     e.rew64);
                 if (l16 == 0) slice_store_scalars<1>(e, env, v);
             }
             // the group's replay rows (lb_replay_add's), once the step's outputs have landed
@@ -108,7 +111,7 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_dqn_step(DSParams d, Params e, 
                 r.rb_next_obs[ps * n4 + j] = nx;
                 r.obs[j] = nx;
             }
-            if (l16 == 0 && env < e.B) {  // (the lane that wrote the env's reward, done and stats row)
+            if (s < P && l16 == 0 && env < e.B) {  // (the lane that wrote the env's reward, done and stats row)
                 const bool dn = e.done[env] != 0;
                 r.rb_actions[ps * e.B + env] = a;
                 r.rb_rewards[ps * e.B + env] = e.reward[env];

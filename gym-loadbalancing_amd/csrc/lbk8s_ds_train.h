@@ -689,6 +689,7 @@ struct DQNHeadParams {
     float* sq_err;  // [M]
     float* td;      // [M] or NULL
     float* old;     // [M] or NULL
+    float* loss;    // [1] or NULL: mean of sq_err (k_dqn_head_block only)
 };
 __global__ __launch_bounds__(256) void k_dqn_head(DQNHeadParams p) {
     const int lane = threadIdx.x & 63;
@@ -712,10 +713,42 @@ __global__ __launch_bounds__(256) void k_dqn_head(DQNHeadParams p) {
     }
 }
 
+// the same head for up to DQN_HEAD_BLOCK_MAX samples in one block, one lane per sample, and
+// the loss (the mean of the squared errors, summed in float64 in a fixed tree) in the same
+// launch: the DQN's 128-sample train step then needs no separate mean kernel
+constexpr int DQN_HEAD_BLOCK_MAX = 1024;
+__global__ __launch_bounds__(DQN_HEAD_BLOCK_MAX) void k_dqn_head_block(DQNHeadParams p) {
+    __shared__ double part[DQN_HEAD_BLOCK_MAX / 64];
+    const int s = threadIdx.x, R = p.R;
+    double sq = 0.0;
+    if (s < p.M) {
+        float m = -INFINITY;
+        for (int r = 0; r < R; ++r) m = fmaxf(m, p.q_next[(int64_t)s * R + r]);
+        const float td = p.rewards[s] + p.gamma * m * (1.f - p.dones[s]);
+        const int a = (int)p.actions[s];
+        const float old = p.q[(int64_t)s * R + a];
+        const float d = td - old;
+        const float g = p.two_over_m * (old - td);
+        for (int r = 0; r < R; ++r) p.dq[(int64_t)s * R + r] = r == a ? g : 0.f;
+        const float e = d * d;
+        p.sq_err[s] = e;
+        if (p.td) p.td[s] = td;
+        if (p.old) p.old[s] = old;
+        sq = (double)e;
+    }
+    for (int o = 32; o > 0; o >>= 1) sq += __shfl_down(sq, o);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = sq;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += part[w];
+        *p.loss = (float)(t / (double)p.M);
+    }
+}
+
 // lb_ds_pack_backward: one thread per image float; transposed fragment order for the
 // 64x64 matrices (lane l of fragment (nt, k) holds W^T[16nt + (l & 15)][in(k, l >> 4)])
-__global__ void k_ds_pack_bwd(lb_ds_weights w, float* out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void ds_pack_bwd_one(const lb_ds_weights& w, float* out, int i) {
     if (i >= DSB_FLOATS) return;
     if (i >= DSB_A3L) {
         const int j = i - DSB_A3L;
@@ -732,6 +765,16 @@ __global__ void k_ds_pack_bwd(lb_ds_weights w, float* out) {
     const int row = 16 * nt + (lane & 15);                        // output of W^T = input of W
     const int in = 16 * (k >> 2) + 4 * (lane >> 4) + (k & 3);     // input of W^T = output of W
     out[i] = src ? src[in * 64 + row] : 0.f;
+}
+__global__ void k_ds_pack_bwd(lb_ds_weights w, float* out) {
+    ds_pack_bwd_one(w, out, blockIdx.x * blockDim.x + threadIdx.x);
+}
+// lb_ds_pack_pair: both images of the same weights in one launch (the first blocks the forward
+// image, the rest the backward image); a DQN train period packs them once at its start
+constexpr int DS_PACK_BLOCKS = (DS_FLOATS + 255) / 256, DSB_PACK_BLOCKS = (DSB_FLOATS + 255) / 256;
+__global__ void k_ds_pack_pair(lb_ds_weights w, float* out, float* bout) {
+    if ((int)blockIdx.x < DS_PACK_BLOCKS) ds_pack_one(w, out, blockIdx.x * 256 + threadIdx.x);
+    else ds_pack_bwd_one(w, bout, (blockIdx.x - DS_PACK_BLOCKS) * 256 + threadIdx.x);
 }
 
 // ---- lb_ds_set_grads: out[m][n] = scale * sum_s A(s, m) B(s, n), one job per weight

@@ -460,9 +460,11 @@ __device__ __forceinline__ double slice_apply(const Params& p, int64_t env, int 
 }
 // get_state() of the step's result: the wave's 4 envs as whole lines through LDS (W = 16), or
 // per env
-template <int W, int EPL, int NWB = BLOCK / 64>  // NWB: waves per block (the LDS stage has one region per wave)
+// NWB: waves per block (the LDS stage has one region per wave); 0: not every slice of the
+// wave steps a live env of the caller's (per-env stores)
+template <int W, int EPL, int NWB = BLOCK / 64>
 __device__ __forceinline__ void slice_obs(const Params& p, int64_t env, int lane, const SEnv<EPL>& v, float* obs_out) {
-    if constexpr (W == 16) {
+    if constexpr (W == 16 && NWB > 0) {
         // whole-line stores of the wave's 4 envs when all 4 are live
         __shared__ float4 obs_stage[NWB][8 * (16 * EPL + 1)];
         const int wl = threadIdx.x & 63;

@@ -171,6 +171,8 @@ def lib():
     L.lb_replay_add.argtypes = [i64, i32, i64] + [vp] * 15 + [vp]
     L.lb_ds_train_forward.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp, vp]
     L.lb_ds_pack_backward.argtypes = [C.POINTER(LBDSWeightsC), vp, vp]
+    L.lb_ds_forward_pair.argtypes = [vp] * 8 + [i64, i32, vp]
+    L.lb_ds_pack_pair.argtypes = [C.POINTER(LBDSWeightsC), vp, vp, vp]
     L.lb_ds_train_backward.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp]
     L.lb_episode_log.argtypes = [i64, vp, vp, vp, vp, vp, vp, vp, i64, vp, i64, vp, vp]
     L.lb_reward64.argtypes = [vp, cfgp, i64, C.POINTER(C.c_void_p)]
@@ -179,7 +181,7 @@ def lib():
                               i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.lb_dqn_steps.argtypes = L.lb_dqn_step.argtypes[:-1] + [i32, vp, vp]
     L.lb_dqn_steps_supported.argtypes = [cfgp, i64, i32]
-    L.lb_dqn_head.argtypes = [vp, vp, vp, vp, vp, i64, i32, C.c_float, vp, vp, vp, vp, vp]
+    L.lb_dqn_head.argtypes = [vp, vp, vp, vp, vp, i64, i32, C.c_float, vp, vp, vp, vp, vp, vp]
     L.lb_replay_sample.argtypes = [i64, i32, i64, i32, C.c_uint64] + [vp] * 12 + [vp]
     L.lb_ds_set_grads.argtypes = [vp, vp, vp, i64, i32, vp, vp]
     for f in ("lb_validate_config", "lb_state_bytes", "lb_init", "lb_reset", "lb_step", "lb_policy", "lb_rollout",
@@ -188,7 +190,7 @@ def lib():
               "lb_ds_train_forward", "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax",
               "lb_replay_add", "lb_ppo_head", "lb_episode_log", "lb_dqn_act", "lb_dqn_head",
               "lb_replay_sample", "lb_ds_set_grads", "lb_dqn_step", "lb_dqn_steps",
-              "lb_dqn_steps_supported"):
+              "lb_dqn_steps_supported", "lb_ds_pack_pair", "lb_ds_forward_pair"):
         getattr(L, f).restype = C.c_int
     v = L.lb_abi_version()
     if v != ABI_VERSION and product:
@@ -219,4 +221,4 @@ EXPORTED_SYMBOLS = ("lb_abi_version", "lb_last_error", "lb_validate_config", "lb
                     "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax", "lb_replay_add", "lb_ppo_head",
                     "lb_episode_log", "lb_dqn_act", "lb_dqn_head", "lb_replay_sample", "lb_ds_set_grads",
                     "lb_rollout_kernel", "lb_source_hash", "lb_reward64", "lb_dqn_step",
-                    "lb_dqn_steps", "lb_dqn_steps_supported")
+                    "lb_dqn_steps", "lb_dqn_steps_supported", "lb_ds_pack_pair", "lb_ds_forward_pair")

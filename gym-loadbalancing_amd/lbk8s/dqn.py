@@ -125,6 +125,12 @@ def dqn_loss(q_network, target_network, obs, actions, next_obs, rewards, dones, 
     device) the TD target, the squared errors and the loss's gradient are one launch
     (fused_train.dqn_head)."""
     if fused.ENABLED and obs.is_cuda and fused_train.supported(q_network.q_network.net, obs):
+        if (obs.shape[1] <= fused_train.PAIR_MAX_ELEMENTS and next_obs.shape == obs.shape and torch.is_grad_enabled()
+                and fused._geometry_ok(target_network.q_network.net, next_obs)):
+            # (the target's Q(next_obs) and the trained forward in one launch)
+            q, q_next = fused_train.q_train_with_target(q_network, q_network.q_network.net, obs, target_network,
+                                                        next_obs)
+            return fused_train.dqn_head(q, q_next, actions, rewards, dones, gamma)
         with torch.no_grad():
             q_next = fused.q_forward(target_network, next_obs)
         return fused_train.dqn_head(q_network(obs), q_next, actions, rewards, dones, gamma)
@@ -215,6 +221,9 @@ class DQN_DeepSets:
         # the target network's image, packed when the target changes (every
         # target_network_frequency steps), outside the captured periods
         self._tfrag = fused.frag_buffer(self.device) if self.device_rng else None
+        # the q network's training-backward image, packed with its forward image at the start
+        # of every train period (lb_ds_pack_pair) and pinned for the run
+        self._qbfrag = fused.bwd_frag_buffer(self.device) if self.device_rng else None
         self._one = None
 
     def select_actions(self, obs, masks, epsilon):
@@ -306,7 +315,8 @@ class DQN_DeepSets:
     def _period_body(self, obs, masks, n, train, parity):
         """n vector steps from `parity` then (train) the sample and the train step; returns
         the graphs' split point for the all_reduce (multi-rank) via self._period_split."""
-        fused.pack_q_into(self.q_network, self._qfrag)
+        # (with the train step, its backward's image of the same weights in the same launch)
+        fused.pack_q_into(self.q_network, self._qfrag, self._qbfrag if train else None)
         self._vector_steps_dev(obs, masks, parity, n)
         if train:
             self._sample_dev(parity ^ (n & 1))
@@ -394,15 +404,39 @@ class DQN_DeepSets:
         # both images are pinned for the run: the q image is packed at the start of every
         # period (the train step's forward reuses it: no repack inside the period), the
         # target's when the target changes
-        fused.pack_q_into(self.q_network, self._qfrag)
+        fused.pack_q_into(self.q_network, self._qfrag, self._qbfrag)
         fused.pack_q_into(self.target_network, self._tfrag)
         fused.pin(self.q_network, self._qfrag)
         fused.pin(self.target_network, self._tfrag)
+        fused.pin_backward(self.q_network, self._qbfrag)
         try:
             return self._learn_device_loop(total_timesteps, start, slope)
         finally:
             fused.pin(self.q_network, None)
             fused.pin(self.target_network, None)
+            fused.pin_backward(self.q_network, None)
+            fused.invalidate(self.q_network)
+            fused.invalidate(self.target_network)
+
+    def prepare(self, total_timesteps):
+        """Capture the period graphs of a learn(total_timesteps) (its exploration slope) without
+        running a step: a following learn() with the same total replays them instead of
+        capturing them inside its own wall time (a one-time cost; benchmarks call this first)."""
+        if not self.period_graph:
+            return
+        slope = self._set_schedule(total_timesteps)
+        if self._pgraphs and self._pgraph_slope == slope:
+            return
+        fused.pin(self.q_network, self._qfrag)
+        fused.pin(self.target_network, self._tfrag)
+        fused.pin_backward(self.q_network, self._qbfrag)
+        try:
+            self._pgraphs = self._build_period_graphs(self._obs, self._masks)
+            self._pgraph_slope = slope
+        finally:
+            fused.pin(self.q_network, None)
+            fused.pin(self.target_network, None)
+            fused.pin_backward(self.q_network, None)
             fused.invalidate(self.q_network)
             fused.invalidate(self.target_network)
 
@@ -501,7 +535,7 @@ class DQN_DeepSets:
         self.optimizer.zero_grad(set_to_none=True)
         # (the seed gradient from a fixed tensor: loss.backward() fills a new one each step)
         if self._one is None or self._one.device != loss.device:
-            self._one = torch.ones((), dtype=loss.dtype, device=loss.device)
+            self._one = fused_train.unit_seed(loss.device, loss.dtype)
         loss.backward(self._one)
         if self._multi and self.train_graph:
             torch.cat([p.grad.reshape(-1) for p in self.q_network.parameters()], out=self._gflat)

@@ -161,14 +161,39 @@ def q_forward_graphable(qnet, x, out, frag):
     return out
 
 
-def pack_q_into(qnet, frag):
+def pack_q_into(qnet, frag, bfrag=None):
     """Pack a DQNDeepSetAgent's live parameters into the fixed image `frag` (one launch;
-    graph-capturable: a replay re-packs the current parameters)."""
+    graph-capturable: a replay re-packs the current parameters); with `bfrag`, the training
+    backward's image too, in the same launch (lb_ds_pack_pair)."""
     w, keep = _weights_struct(qnet.q_network.net, None)
-    _native.check(_native.lib().lb_ds_pack(C.byref(w), frag.data_ptr(),
-                                           torch.cuda.current_stream(frag.device).cuda_stream))
+    stream = torch.cuda.current_stream(frag.device).cuda_stream
+    if bfrag is None:
+        _native.check(_native.lib().lb_ds_pack(C.byref(w), frag.data_ptr(), stream))
+    else:
+        _native.check(_native.lib().lb_ds_pack_pair(C.byref(w), frag.data_ptr(), bfrag.data_ptr(), stream))
     del keep
     return frag
+
+
+def bwd_frag_buffer(device):
+    """A fixed backward weight-image buffer (pack_q_into's bfrag)."""
+    return torch.empty(_native.LB_DS_BWD_FLOATS, dtype=torch.float32, device=device)
+
+
+_pinned_bwd = weakref.WeakKeyDictionary()
+
+
+def pin_backward(module, bfrag):
+    """As pin(), for the training backward's image of `module` (fused_train): the caller keeps
+    `bfrag` current.  pin_backward(module, None) undoes it."""
+    if bfrag is None:
+        _pinned_bwd.pop(module, None)
+    else:
+        _pinned_bwd[module] = bfrag
+
+
+def pinned_backward(module):
+    return _pinned_bwd.get(module)
 
 
 @torch.no_grad()

@@ -115,7 +115,7 @@ class _FusedDeepSetsTrain(torch.autograd.Function):
         _native.check(_native.lib().lb_ds_train_forward(
             frag.data_ptr(), x.data_ptr(), B, R, logits.data_ptr(), fused._ptr(mean), save_a.data_ptr(),
             fused._ptr(save_c), setvec.data_ptr(), _stream(dev)))
-        ctx.actor_net, ctx.critic = actor_net, critic
+        ctx.actor_net, ctx.critic, ctx.owner = actor_net, critic, owner
         ctx.save_for_backward(x, save_a, save_c, setvec)
         if critic is None:
             return logits
@@ -132,7 +132,9 @@ class _FusedDeepSetsTrain(torch.autograd.Function):
         dlogits = dlogits.float().contiguous()
         if critic is not None:
             dmean = torch.zeros((B, 64), dtype=torch.float32, device=dev) if dmean is None else dmean.float().contiguous()
-        bfrag = _pack_backward(actor_net, critic, dev)
+        bfrag = fused.pinned_backward(ctx.owner)  # (a DQN train period packs it with the forward's)
+        if bfrag is None:
+            bfrag = _pack_backward(actor_net, critic, dev)
         wgrad = torch.empty((2, _native.LB_DS_WGRAD_FLOATS), dtype=torch.float32, device=dev)
         work = _workspace(dev)
         _native.check(_native.lib().lb_ds_train_backward(
@@ -170,6 +172,48 @@ class _FusedDeepSetsTrain(torch.autograd.Function):
                 _over_sets(dmean, _vec(setvec, "MAX2C"), -1.0),                # critic Gamma3
             ]
         return (None, None, None, None) + tuple(grads)
+
+
+class _FusedQTrainWithTarget(_FusedDeepSetsTrain):
+    """(x, owner, actor_net, tfrag, x_next, *params) -> (logits (B, R), q_next (B, R)): the
+    actor-only training forward of _FusedDeepSetsTrain and, in the same launch
+    (lb_ds_forward_pair), the Q values of x_next under the packed image tfrag (the DQN's
+    target network; no gradient).  The backward is _FusedDeepSetsTrain's."""
+
+    @staticmethod
+    def forward(ctx, x, owner, actor_net, tfrag, x_next, *params):
+        dev = x.device
+        B, R, _ = x.shape
+        frag = fused.packed(owner, actor_net, None)
+        logits = torch.empty((B, R), dtype=torch.float32, device=dev)
+        q_next = torch.empty((B, R), dtype=torch.float32, device=dev)
+        save_a = torch.empty((2, B, R, 64), dtype=torch.float32, device=dev)
+        setvec = torch.empty((B, SV), dtype=torch.float32, device=dev)
+        _native.check(_native.lib().lb_ds_forward_pair(
+            tfrag.data_ptr(), x_next.data_ptr(), q_next.data_ptr(), frag.data_ptr(), x.data_ptr(), logits.data_ptr(),
+            save_a.data_ptr(), setvec.data_ptr(), B, R, _stream(dev)))
+        ctx.actor_net, ctx.critic, ctx.owner = actor_net, None, owner
+        ctx.save_for_backward(x, save_a, None, setvec)
+        ctx.mark_non_differentiable(q_next)
+        ctx.set_materialize_grads(False)
+        return logits, q_next
+
+    @staticmethod
+    def backward(ctx, dlogits, dq_next=None):
+        grads = _FusedDeepSetsTrain.backward(ctx, dlogits)
+        return (None,) * 5 + tuple(grads[4:])
+
+
+PAIR_MAX_ELEMENTS = 16  # lb_ds_forward_pair's sets
+
+
+def q_train_with_target(owner, actor_net, x, target, x_next):
+    """DQN train step forwards in one launch: (Q(x) of `owner`'s actor_net, differentiable;
+    Q(x_next) of the DQNDeepSetAgent `target`, no gradient)."""
+    x = x.float().contiguous()
+    x_next = x_next.float().contiguous()
+    tfrag = fused.packed(target, target.q_network.net, None)
+    return _FusedQTrainWithTarget.apply(x, owner, actor_net, tfrag, x_next, *_eq_params(actor_net))
 
 
 class _Rho(torch.autograd.Function):
@@ -254,6 +298,8 @@ class _PPOHead(torch.autograd.Function):
         dlogits, dvalue = ctx.saved_tensors
         if gloss is None:
             return (None,) * 12
+        if is_unit_seed(gloss):  # (x * 1 == x bit for bit: no multiply launches)
+            return (dlogits, dvalue.view(ctx.vshape)) + (None,) * 10
         return (dlogits * gloss, (dvalue * gloss).view(ctx.vshape)) + (None,) * 10
 
 
@@ -277,24 +323,44 @@ class _DQNHead(torch.autograd.Function):
         sq = torch.empty((M,), dtype=torch.float32, device=dev)
         td = torch.empty((M,), dtype=torch.float32, device=dev)
         old = torch.empty((M,), dtype=torch.float32, device=dev)
+        # (up to 1024 samples the kernel also takes the mean: no separate reduction launch)
+        loss = torch.empty((), dtype=torch.float32, device=dev) if M <= DQN_HEAD_LOSS_MAX else None
         keep = [q_next.float().contiguous(), actions.reshape(-1).to(torch.int64).contiguous(),
                 rewards.reshape(-1).float().contiguous(), dones.reshape(-1).float().contiguous()]
         _native.check(_native.lib().lb_dqn_head(
             q.data_ptr(), *[t.data_ptr() for t in keep], M, R, float(gamma), dq.data_ptr(), sq.data_ptr(),
-            td.data_ptr(), old.data_ptr(), _stream(dev)))
+            td.data_ptr(), old.data_ptr(), fused._ptr(loss), _stream(dev)))
         ctx.save_for_backward(dq)
         ctx.mark_non_differentiable(td, old)
         # (td and old get no gradient: without this autograd fills two zero tensors for them,
         # two kernels per DQN train step)
         ctx.set_materialize_grads(False)
-        return sq.mean(), td, old
+        return (sq.mean() if loss is None else loss), td, old
 
     @staticmethod
     def backward(ctx, gloss, gtd, gold):
         (dq,) = ctx.saved_tensors
         if gloss is None:
             return (None,) * 6
+        if is_unit_seed(gloss):  # (dq * 1 == dq bit for bit: no multiply launch)
+            return dq, None, None, None, None, None
         return dq * gloss, None, None, None, None, None
+
+
+DQN_HEAD_LOSS_MAX = 1024  # lb_dqn_head's one-block loss (loss_out)
+
+
+def unit_seed(device, dtype=torch.float32):
+    """A scalar 1 to seed loss.backward() with; the loss heads' backward recognise it (autograd
+    hands the root's seed tensor itself to the head) and return their saved gradient as is
+    instead of launching a multiply by 1."""
+    t = torch.ones((), dtype=dtype, device=device)
+    t._lbk8s_unit = True
+    return t
+
+
+def is_unit_seed(g):
+    return getattr(g, "_lbk8s_unit", False)
 
 
 def dqn_head(q, q_next, actions, rewards, dones, gamma):

@@ -29,7 +29,7 @@ import torch
 from torch import nn, optim
 
 from . import dist as lbdist
-from . import fused
+from . import fused, fused_train
 from .deepsets import DeepSetAgent
 
 
@@ -205,7 +205,11 @@ class PPO_DeepSets:
         # pool, at the same addresses every replay, and no zero fill + accumulate per parameter
         # is recorded)
         self.optimizer.zero_grad(set_to_none=True)
-        out[0].backward()
+        # (a fixed unit seed: the fused loss head returns its saved gradients as they are)
+        seed = getattr(self, "_seed1", None)
+        if seed is None or seed.device != out[0].device or seed.dtype != out[0].dtype:
+            seed = self._seed1 = fused_train.unit_seed(out[0].device, out[0].dtype)
+        out[0].backward(seed)
         if self._multi:
             torch.cat([p.grad.reshape(-1) for p in self.agent.parameters()], out=self._gflat)
         return out

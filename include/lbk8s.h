@@ -328,10 +328,11 @@ int lb_dqn_steps(const float* frag, float* obs, int64_t num_envs, int32_t num_el
 /* DQN loss head (dqn_deepset.py:180-187): per sample td = r + gamma max q_next (1 - done),
  * sq_err_out = (td - q[a])^2 (mean = F.mse_loss) and dq_out = d mean / d q (2 (q[a] - td) /
  * M at column a, 0 elsewhere); td_out / old_out (may be NULL) the TD target and q[a].
- * q, q_next [M,R] f32; actions [M] int64; rewards, dones [M]. */
+ * q, q_next [M,R] f32; actions [M] int64; rewards, dones [M].  loss_out (may be NULL; ABI 10):
+ * the mean of the squared errors, in the same launch (num_sets <= 1024; float64 sum). */
 int lb_dqn_head(const float* q, const float* q_next, const int64_t* actions, const float* rewards, const float* dones,
                 int64_t num_sets, int32_t num_elements, float gamma, float* dq_out, float* sq_err_out, float* td_out,
-                float* old_out, void* stream);
+                float* old_out, float* loss_out, void* stream);
 
 /* Replay sample (SB3 ReplayBuffer.sample, :177): `batch` draws of (slot, env) uniform over
  * slot < min(*base_adds + *vstep, slots) and env < num_envs (Philox keyed by seed, counter
@@ -412,6 +413,14 @@ int lb_ds_train_forward(const float* frag, const float* obs, int64_t num_envs, i
                         float* logits_out, float* psi_mean_out, float* save_actor, float* save_critic,
                         float* setvec_out, void* stream);
 
+/* Two actor-only forwards in ONE launch (ABI 10; R = num_elements <= 16): lb_ds_forward(frag_a,
+ * obs_a -> logits_a) and lb_ds_train_forward(frag_b, obs_b -> logits_b, save_actor_b,
+ * setvec_b), the same batch size -- the DQN train step's target Q values of the next
+ * observations and the trained network's forward (envs/dqn_deepset.py:180-186). */
+int lb_ds_forward_pair(const float* frag_a, const float* obs_a, float* logits_a, const float* frag_b,
+                       const float* obs_b, float* logits_b, float* save_actor_b, float* setvec_b, int64_t num_envs,
+                       int32_t num_elements, void* stream);
+
 /* PPO loss head (envs/ppo_deepset.py:227-263) for M sets of R <= 257 elements: per-set
  * terms [M,6] (policy term max(pg1, pg2), value term, entropy, approx-kl term, clipped
  * indicator, loss term = pg - ent_coef H + vf_coef/2 v; their means are the reference's
@@ -425,6 +434,8 @@ int lb_ppo_head(const float* logits, const uint8_t* masks, const float* actions,
 
 /* Pack the backward image [LB_DS_BWD_FLOATS] (transposed layer-2/3 matrices). */
 int lb_ds_pack_backward(const lb_ds_weights* w, float* bwd_frag_out, void* stream);
+/* lb_ds_pack and lb_ds_pack_backward of the same weights in one launch (ABI 10). */
+int lb_ds_pack_pair(const lb_ds_weights* w, float* frag_out, float* bwd_frag_out, void* stream);
 
 /* dlogits [B,R] (NULL = no actor), dmean [B,64] (NULL = no critic) -> wgrad_out
  * [2, LB_DS_WGRAD_FLOATS] (actor, critic: dLambda2, dLambda1; a head not asked for gets

