@@ -531,9 +531,21 @@ int device_cus() {
     return cus;
 }
 
-// k_rollout_lean: one 64-thread block per 64-env group (B % 64 == 0)
+// k_rollout_lean: one 64-thread block per 64-env group (B % 64 == 0).  Launches of at most
+// LEAN_SPLIT_MAX_K steps pair each env wave with a copy wave in a 128-thread block
+// (k_rollout_lean_split, lbk8s_lean.h: lean_copier): 3-4% faster at K = 20 (131,072 and 2^20
+// envs), 1-2% slower at K = 100 (profiles/r05_ab_split.jsonl)
+#ifndef LB_LEAN_SPLIT_MAX_K
+#define LB_LEAN_SPLIT_MAX_K 32
+#endif
+constexpr int LEAN_SPLIT_MAX_K = LB_LEAN_SPLIT_MAX_K;
 template <int KIND, int ET, int RT, int NZW, bool NAIVE, bool ACT>
 void launch_lean(const Params& p, int64_t B, int steps, int32_t* act, hipStream_t s) {
+    if (steps <= LEAN_SPLIT_MAX_K) {
+        hipLaunchKernelGGL((k_rollout_lean_split<KIND, ET, RT, NZW, NAIVE, ACT, 1>), dim3((unsigned)(B / 64)), dim3(128), 0,
+                           s, p, steps, act);
+        return;
+    }
     hipLaunchKernelGGL((k_rollout_lean<KIND, ET, RT, NZW, NAIVE, ACT>), dim3((unsigned)((B + LEAN_NB - 1) / LEAN_NB)),
                        dim3(LEAN_NB), 0, s, p, steps, act);
 }

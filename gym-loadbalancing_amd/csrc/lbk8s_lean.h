@@ -516,20 +516,74 @@ constexpr int LTL_NP = 6, LTL_H = 8;  // per wave: 8 header words, then 6 stamps
 #endif
 constexpr int LEAN_NB = LB_LEAN_NB;
 
-template <int KIND, int ET, int RT, int NZW, bool NAIVE, bool ACT>
-__global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p, int K, int32_t* act_out) {
-    constexpr int NB = LEAN_NB, NW = NB / 64, P = 2 * RT, GT = 64 / P;
+// The split layout (CW = 1: k_rollout_lean_split, lb_rollout's launches of at most
+// LEAN_SPLIT_MAX_K steps): each block pairs the env wave with a copy wave.  The env wave never
+// issues an observation store: at each step it leaves the step's reward / done (/ action)
+// words next to its image and meets the copy wave at two LDS-only barriers, A (image and words
+// ready) and B (the copy wave has read them into its registers); between them it prepares the
+// next step.  The copy wave then issues the step's obs block, reward and done stores while the
+// env wave computes.  (The env work alone runs 26-30 us per step at 2^20 envs, the store stream
+// alone 46-55, the two in one wave 63-66; split, the env waves are half as many per SIMD, and
+// the 20-step launch gains 3-4%, the 100-step one loses 1-2%: profiles/r05_ab_split.jsonl.)
+template <int P, bool ACT, int CW>
+__device__ __forceinline__ void lean_copier(const Params& p, int K, int32_t* act_out, uint32_t (*simg)[64 * IMG_W],
+                                            const uint32_t* sst, int64_t env0) {
+    const int lane = threadIdx.x & 63;
+    const bool h = (lane & 1) != 0;
+    for (int k = 0; k < K; ++k) {
+        block_lds_sync();  // A: step k's images and words are in LDS
+        float4 v[CW][P];
+        uint32_t rw[CW], dn[CW], ac[CW];
+#pragma unroll
+        for (int c = 0; c < CW; ++c) {
+#pragma unroll
+            for (int it = 0; it < P; ++it) v[c][it] = lean_piece<P>(simg[c], lane, it, h);
+            rw[c] = sst[192 * c + lane];
+            dn[c] = sst[192 * c + 64 + lane];
+            ac[c] = ACT ? sst[192 * c + 128 + lane] : 0u;
+        }
+        block_lds_sync();  // B: read (the env waves may rewrite them)
+        const Rsrc out = rsrc_of(p.obs + (int64_t)k * p.B * (P / 2) * 8);
+        const Rsrc rwo = rsrc_of(p.reward + (int64_t)k * p.B), dno = rsrc_of(p.done + (int64_t)k * p.B);
+#pragma unroll
+        for (int c = 0; c < CW; ++c) {
+            const uint32_t envi = (uint32_t)(env0 + 64 * c + lane);
+            const uint32_t obs_wave = (uint32_t)((env0 + 64 * c) * P * 16);
+#pragma unroll
+            for (int it = 0; it < P; ++it)
+                buf_st_f4<BUF_NT>(v[c][it], out, (uint32_t)lane * 16u + obs_wave + 1024u * (uint32_t)it);
+            __builtin_amdgcn_raw_buffer_store_b32(rw[c], rwo, envi * 4u, 0, BUF_NT);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)dn[c], dno, envi, 0, BUF_NT);
+            if (ACT) __builtin_amdgcn_raw_buffer_store_b32(ac[c], rsrc_of(act_out + (int64_t)k * p.B), envi * 4u, 0, 0);
+        }
+    }
+}
+
+// (the LDS arrays are the kernels': LDS declared in a device function is lowered as
+// module-level, and the compiler then assumes occupancy 1 and spends registers accordingly)
+template <int KIND, int ET, int RT, int NZW, bool NAIVE, bool ACT, int CW>
+__device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uint32_t (*simg)[64 * IMG_W],
+                                          uint32_t* sstage) {
+    static_assert(CW == 0 || CW == 1, "one env wave per copy wave (two: the copy wave's registers for both blocks spilled)");
+    constexpr bool SPLIT = CW > 0;
+    constexpr int NB = SPLIT ? 64 * (CW + 1) : LEAN_NB, NW = SPLIT ? CW : NB / 64, P = 2 * RT, GT = 64 / P;
     constexpr int FAST = GT < REC_FETCH_MAX ? GT : REC_FETCH_MAX;  // restarts per step of the fast path
     static_assert(ET >= 1 && ET <= TPE_E && (RT == ET || RT == ET + 1), "compile-time geometry");
-    __shared__ __attribute__((aligned(16))) uint32_t simg[NW][64 * IMG_W];
+    (void)NW;
     const LDims<ET, RT> d(p);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if constexpr (SPLIT) {
+        if (wv == CW) {  // the copy wave (its block's env waves 0 .. CW - 1: envs blockIdx.x * 64 CW ..)
+            lean_copier<P, ACT, CW>(p, K, act_out, simg, sstage, (int64_t)blockIdx.x * 64 * CW);
+            return;
+        }
+    }
     uint32_t* wimg = simg[wv];
     uint32_t* me = wimg + lane * IMG_W;
     // whole waves only (the host checks B % 64 == 0): every lane of a live wave is a live env,
     // and the waves past B in a partial last block leave (no block barrier follows: every
-    // synchronisation below is within the wave)
-    const int64_t env0 = (int64_t)blockIdx.x * NB + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63);
+    // synchronisation below is within the wave; the split layout's blocks are whole)
+    const int64_t env0 = (int64_t)blockIdx.x * (SPLIT ? 64 * CW : NB) + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63);
     if (env0 >= p.B) return;
 #ifdef LB_TIMELINE
     if (g_timeline && threadIdx.x % 64 == 0)
@@ -793,6 +847,19 @@ __global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p
             }
         }
         LB_LTL(k, 2);
+        if constexpr (SPLIT) {  // the copy wave stores step k's outputs
+            sstage[192 * wv + lane] = __float_as_uint((float)reward);
+            sstage[192 * wv + 64 + lane] = done ? 1u : 0u;
+            if (ACT) sstage[192 * wv + 128 + lane] = (uint32_t)a_k;
+            block_lds_sync();  // A
+            if (k + 1 < K) {
+                pr = prep([](int) {});
+                asm volatile("" : "+v"(pr.sel_lat), "+v"(pr.sel_cpu), "+v"(pr.next_lat), "+v"(pr.next_cpu),
+                             "+v"(qn.x), "+v"(qn.y), "+v"(qn.z), "+v"(qn.w));
+            }
+            block_lds_sync();  // B (the image and words are read)
+            return;
+        }
         // step k's outputs leave after step k + 1's gathers, spread over its request draws
         const Rsrc out = rsrc_of(p.obs + k * (int64_t)p.B * RT * 8);
         const Rsrc rw = rsrc_of(p.reward + (int64_t)k * p.B), dn = rsrc_of(p.done + (int64_t)k * p.B);
@@ -906,6 +973,23 @@ __global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p
 #ifdef LB_TIMELINE
     if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP) + 3] = __builtin_amdgcn_s_memrealtime();
 #endif
+}
+
+template <int KIND, int ET, int RT, int NZW, bool NAIVE, bool ACT>
+__global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p, int K, int32_t* act_out) {
+    __shared__ __attribute__((aligned(16))) uint32_t simg[LEAN_NB / 64][64 * IMG_W];
+    lean_body<KIND, ET, RT, NZW, NAIVE, ACT, 0>(p, K, act_out, simg, nullptr);
+}
+// the split layout: 128-thread blocks (env wave + copy wave)
+#ifndef LB_LEAN_SPLIT_LB
+#define LB_LEAN_SPLIT_LB 4  // (min waves per SIMD: 128 VGPRs)
+#endif
+template <int KIND, int ET, int RT, int NZW, bool NAIVE, bool ACT, int CW>
+__global__ __launch_bounds__(64 * (CW + 1), LB_LEAN_SPLIT_LB) void k_rollout_lean_split(Params p, int K,
+                                                                                       int32_t* act_out) {
+    __shared__ __attribute__((aligned(16))) uint32_t simg[CW][64 * IMG_W];
+    __shared__ uint32_t sstage[CW * 3 * 64];  // each env wave's step reward, done, action words
+    lean_body<KIND, ET, RT, NZW, NAIVE, ACT, CW>(p, K, act_out, simg, sstage);
 }
 
 }  // namespace lbk

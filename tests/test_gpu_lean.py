@@ -52,7 +52,7 @@ def _compare_after(a_env, b_env, B):
     (65536 + 320, dict(num_endpoints=6, reward_function="multi")),  # E = 6, N = 24: one node-zone word
 ])
 @pytest.mark.parametrize("kind", ["random", "topo", "zone_cpu", "endpoint_cpu"])
-@pytest.mark.parametrize("K,L", [(20, 20), (13, 20), (7, 9)])
+@pytest.mark.parametrize("K,L", [(20, 20), (13, 20), (7, 9), (40, 40)])  # (40: the single-wave layout)
 def test_lean_staggered_equals_policy_plus_step(B, kw, kind, K, L):
     """Staggered episodes (1/L of the envs end at every step; some waves have more enders
     in a step than the prefetch covers, so both restart paths run), actions written."""

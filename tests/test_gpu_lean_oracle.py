@@ -32,11 +32,14 @@ def _orc_policy(orc, kind):
     return orc.policy_random() if kind == "random" else orc.policy_greedy(ORC_KIND[kind])
 
 
-@pytest.mark.parametrize("B,cfg", [(131072, c) for c in CFGS] + [(65600, "default"), (65600, "cfg1_multi")])
+# K <= 32: the split layout (an env wave and a copy wave per block, k_rollout_lean_split);
+# K = 40: the single-wave layout (lbk8s.hip: LEAN_SPLIT_MAX_K)
+@pytest.mark.parametrize("B,cfg,K", [(131072, c, 20) for c in CFGS] + [(65600, "default", 20), (65600, "cfg1_multi", 20),
+                                                                      (65600, "default", 40), (65600, "cfg1_multi", 40)])
 @pytest.mark.parametrize("kind", ["random", "topo", "zone_cpu", "endpoint_cpu"])
-def test_lean_rollout_equals_oracle(oracle_mod, B, cfg, kind):
+def test_lean_rollout_equals_oracle(oracle_mod, B, cfg, K, kind):
     from lbk8s import LBVecEnv
-    K = L = 20
+    L = K
     seed = 1000 + B % 977
     kw = dict(CFGS[cfg], episode_length=L)
     env = LBVecEnv(B, seed=seed, as_tensors=True, **kw)

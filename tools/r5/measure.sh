@@ -29,6 +29,11 @@ done
 for n in 131072 262144 524288 1048576; do
   $T 300 python3 bench.py --weak --envs $n --steps 20 --warmup 5 --no-cpu-baseline --no-step-line >> gpurun_out/r05_strong_sizes_k20.jsonl 2>>gpurun_out/r05_bench.err || exit 1
 done
+for n in 131072 262144; do
+  $T 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r05_prof_shard_$n -o run --output-format csv -- \
+      python3 bench.py --weak --envs $n --steps 20 --warmup 5 --no-cpu-baseline --no-step-line \
+      > gpurun_out/r05_shard_${n}_under_rocprof.json 2>>gpurun_out/r05_bench.err || exit 1
+done
 $T 400 python3 bench.py --config e64_multi --steps 300 --warmup 100 --no-cpu-baseline > gpurun_out/r05_bench_e64.json 2>>gpurun_out/r05_bench.err || exit 1
 python3 - <<'PY'
 import json

@@ -56,46 +56,50 @@ int main() {
                launches, us, bytes / us / 1e6);
         fflush(stdout);
     };
-    for (int K : {10, 20, 40, 60, 100}) {
-        for (int mode = 0; mode < 3; ++mode) {
-            // mode 0: the same K slots every launch; 1: consecutive launches walk the ring; 2: 4-wave blocks
-            int k0 = 0;
-            auto launch = [&]() {
-                if (mode == 2)
-                    hipLaunchKernelGGL((k_write<4>), dim3((unsigned)(B / 256)), dim3(256), 0, 0, obs, rew, done, B, P, K, k0, T);
-                else
-                    hipLaunchKernelGGL((k_write<1>), dim3((unsigned)(B / 64)), dim3(64), 0, 0, obs, rew, done, B, P, K, k0, T);
-                if (mode == 1) k0 = (k0 + K) % T;
-            };
-            launch();
-            CK(hipDeviceSynchronize());
-            float best = 1e30f;
-            for (int r = 0; r < 5; ++r) {
-                CK(hipEventRecord(a));
-                launch();
-                CK(hipEventRecord(b));
-                CK(hipEventSynchronize(b));
-                float ms;
-                CK(hipEventElapsedTime(&ms, a, b));
-                best = ms < best ? ms : best;
+    // K = 20 by where the timed launch writes: the slots the previous launch wrote ("same"),
+    // slots last written 2 / 5 launches before (a 40 / 100-slot ring), or never-written memory
+    // (a 48 GB region walked once)
+    {
+        const int K = 20;
+        const long FRESH_SLOTS = 160;  // 48 GB of obs at 2^20 envs
+        float4* big;
+        CK(hipMalloc(&big, (size_t)FRESH_SLOTS * B * P * 16));
+        for (int rep = 0; rep < 2; ++rep) {
+            for (int mode = 0; mode < 4; ++mode) {
+                const int TT = mode == 0 ? K : mode == 1 ? 2 * K : 100;
+                int k0 = 0;
+                long fresh = 0;
+                auto launch = [&]() {
+                    if (mode == 3) {
+                        hipLaunchKernelGGL((k_write<1>), dim3((unsigned)(B / 64)), dim3(64), 0, 0, big + fresh * B * P, rew,
+                                           done, B, P, K, 0, T);
+                        fresh += K;
+                    } else {
+                        hipLaunchKernelGGL((k_write<1>), dim3((unsigned)(B / 64)), dim3(64), 0, 0, obs, rew, done, B, P, K,
+                                           k0, TT);
+                        k0 = (k0 + K) % TT;
+                    }
+                };
+                for (int w = 0; w < 5; ++w) launch();  // (fresh: the first 100 slots written)
+                CK(hipDeviceSynchronize());
+                float best = 1e30f, sum = 0.f;
+                for (int r = 0; r < 3; ++r) {
+                    CK(hipEventRecord(a));
+                    launch();
+                    CK(hipEventRecord(b));
+                    CK(hipEventSynchronize(b));
+                    float ms;
+                    CK(hipEventElapsedTime(&ms, a, b));
+                    best = ms < best ? ms : best;
+                    sum += ms;
+                }
+                report(mode == 0 ? "K=20: the slots of the previous launch" : mode == 1 ? "K=20: slots written 2 launches before"
+                       : mode == 2 ? "K=20: slots written 5 launches before" : "K=20: never-written memory", K, best, 1);
+                report(mode == 0 ? "  mean of 3" : mode == 1 ? "  mean of 3" : mode == 2 ? "  mean of 3" : "  mean of 3", K,
+                       sum / 3, 1);
             }
-            report(mode == 0 ? "same slots" : mode == 1 ? "ring walk" : "4-wave blocks", K, best, 1);
         }
-        // back-to-back launches walking the ring, timed together
-        {
-            int k0 = 0;
-            CK(hipDeviceSynchronize());
-            CK(hipEventRecord(a));
-            for (int r = 0; r < 5; ++r) {
-                hipLaunchKernelGGL((k_write<1>), dim3((unsigned)(B / 64)), dim3(64), 0, 0, obs, rew, done, B, P, K, k0, T);
-                k0 = (k0 + K) % T;
-            }
-            CK(hipEventRecord(b));
-            CK(hipEventSynchronize(b));
-            float ms;
-            CK(hipEventElapsedTime(&ms, a, b));
-            report("5 launches back to back, ring walk", K, ms, 5);
-        }
+        CK(hipFree(big));
     }
     return 0;
 }
