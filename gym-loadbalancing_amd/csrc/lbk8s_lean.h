@@ -530,6 +530,27 @@ __device__ __forceinline__ void lean_copier(const Params& p, int K, int32_t* act
                                             const uint32_t* sst, int64_t env0) {
     const int lane = threadIdx.x & 63;
     const bool h = (lane & 1) != 0;
+    // the next episodes of the block's envs that end inside the launch, into their records (the
+    // env wave's prologue in the single-wave layout; here beside the env wave's state loads and
+    // image): 8 lanes per record, 8 records per pass, then barrier P
+#pragma unroll
+    for (int c = 0; c < CW; ++c) {
+        const int64_t env = env0 + 64 * c + lane;
+        const uint64_t sc = p.sc[env], acc3 = p.acc3[env];
+        const int to_done = p.L - (int)(sc & 0xFFFF);
+        uint64_t mm = __ballot(to_done >= 1 && to_done <= K);
+        const uint32_t epi = (uint32_t)(acc3 >> 32) + 1;
+        const int g = lane / RS_W, gl = lane % RS_W;
+        while (mm) {  // (wave-uniform)
+            const int el = nth_env8(mm, g);
+            const uint32_t ep = (uint32_t)__shfl((int)epi, el < 0 ? 0 : el);
+            if (el >= 0) lean_write_record<RS_W>(p, env0 + 64 * c + el, ep, gl);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) mm &= mm - 1;
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the records are written before P)
+    block_lds_sync();  // P
     for (int k = 0; k < K; ++k) {
         block_lds_sync();  // A: step k's images and words are in LDS
         float4 v[CW][P];
@@ -638,8 +659,9 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
         v.dt = 0.f;
     }
 
-    // the next episodes of the envs that end inside the launch, into their records
-    {
+    // the next episodes of the envs that end inside the launch, into their records (split
+    // layout: the copy wave draws them)
+    if constexpr (!SPLIT) {
         const int to_done = p.L - (int)(v.s0 & 0xFFFF);
         const bool fin = to_done >= 1 && to_done <= K;
         const uint64_t fm = __ballot(fin);
@@ -770,6 +792,7 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
         between(5);
         return r;
     };
+    if constexpr (SPLIT) block_lds_sync();  // P: the copy wave's records are written (the prefetch below reads them)
     pr = prep([](int) {});
     // (its loads land here, before the loop: pending at the loop header, they made every
     // wait for the preparation's values inside the loop a vmcnt(0) or close to it)
