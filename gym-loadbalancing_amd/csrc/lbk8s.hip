@@ -569,7 +569,7 @@ int rollout_kernel(const lb_config* c, int64_t B, int32_t steps, bool outputs_al
                             (c->num_endpoints == 6 && R == 7 && c->num_nodes <= 64);
     if (lean_fits && lean_shape && B % 64 == 0 && B > SMALL_TPE_MAX_B && outputs_all &&
         g_rollout_variant == 0)
-        return LB_ROLLOUT_LEAN;
+        return steps <= LEAN_SPLIT_MAX_K ? LB_ROLLOUT_LEAN_SPLIT : LB_ROLLOUT_LEAN;
     if (img_fits && g_rollout_variant != 3) return LB_ROLLOUT_IMG;
     return LB_ROLLOUT_TPE;
 }
@@ -741,7 +741,7 @@ int lb_rollout(void* state, const lb_config* cfg, int64_t num_envs, int32_t poli
         const bool pre = cfg->auto_reset && cfg->episode_length >= steps;
         const int rk = rollout_kernel(cfg, num_envs, steps, obs_out && reward_out && done_out && terminal_obs_out &&
                                                                 ep_stats_out);
-        if (rk == LB_ROLLOUT_LEAN) {  // k_rollout_lean (lbk8s_lean.h): LEAN_NB-thread blocks, B % 64 == 0
+        if (rk == LB_ROLLOUT_LEAN || rk == LB_ROLLOUT_LEAN_SPLIT) {  // k_rollout_lean(_split) (lbk8s_lean.h), B % 64 == 0
             const bool e8 = p.E == 8, naive = p.reward_fn == LB_REWARD_NAIVE, act = actions_out != nullptr;
 #define LB_LEAN(KIND_, ET_, RT_, NZW_)                                                                           \
             if (naive && act) launch_lean<KIND_, ET_, RT_, NZW_, true, true>(p, num_envs, (int)steps, actions_out, s); \

@@ -22,7 +22,7 @@ LB_RNG_PHILOX, LB_RNG_TRACE = 0, 1
 LB_POLICY = {"topo": 0, "zone_cpu": 1, "endpoint_cpu": 2, "random": 3}
 # lb_rollout_kernel's answers (include/lbk8s.h LB_ROLLOUT_*)
 LB_ROLLOUT = {0: "k_rollout_lean", 1: "k_rollout_img", 2: "k_rollout_tpe", 3: "policy+step launches",
-              4: "k_rollout_slice"}
+              4: "k_rollout_slice", 5: "k_rollout_lean_split"}
 LB_FIELD = {"endpoint_latency": 0, "endpoint_cpu_usage_percentage": 1,
             "endpoint_topology_latency": 2, "endpoint_zone_cpu_capacity": 3, "endpoint_zone": 4,
             "endpoint_node": 5, "avg_load_served": 6, "current_time": 7, "current_step": 8,

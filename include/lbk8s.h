@@ -195,9 +195,12 @@ int lb_rollout(void* state, const lb_config* cfg, int64_t num_envs, int32_t poli
  *   LB_ROLLOUT_TPE    k_rollout_tpe (64-bit offsets; also L < K or no auto-reset)
  *   LB_ROLLOUT_STEPS  K policy + step launches (thread-per-env, N > 64)
  *   LB_ROLLOUT_SLICE  k_rollout_slice
+ *   LB_ROLLOUT_LEAN_SPLIT  k_rollout_lean_split: LB_ROLLOUT_LEAN's shapes at K <= 32 steps (an env
+ *                          wave and a copy wave per block; ABI 10)
  * The LEAN / IMG kernels address with 32-bit byte offsets from scalar bases; above 4 GiB of
  * state (or of ep_stats rows, or of one obs slot for LEAN) lb_rollout takes LB_ROLLOUT_TPE. */
-enum { LB_ROLLOUT_LEAN = 0, LB_ROLLOUT_IMG = 1, LB_ROLLOUT_TPE = 2, LB_ROLLOUT_STEPS = 3, LB_ROLLOUT_SLICE = 4 };
+enum { LB_ROLLOUT_LEAN = 0, LB_ROLLOUT_IMG = 1, LB_ROLLOUT_TPE = 2, LB_ROLLOUT_STEPS = 3, LB_ROLLOUT_SLICE = 4,
+       LB_ROLLOUT_LEAN_SPLIT = 5 };
 int lb_rollout_kernel(const lb_config* cfg, int64_t num_envs, int32_t steps, int32_t outputs_all,
                       int32_t* kernel_out);
 

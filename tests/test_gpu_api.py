@@ -330,7 +330,8 @@ def test_rollout_tpe_staggered_equals_policy_plus_step(B, kw, kind, K, L):
             e.reset_masked((gid % L) == r)
     a_env, b_env = envs
     lean = B % 64 == 0 and B > 65536 and kw.get("num_endpoints", 8) in (6, 8)
-    assert a_env.rollout_kernel(K) == ("k_rollout_tpe" if L < K else "k_rollout_lean" if lean else "k_rollout_img")
+    assert a_env.rollout_kernel(K) == ("k_rollout_tpe" if L < K else ("k_rollout_lean_split" if K <= 32 else "k_rollout_lean") if lean
+                                          else "k_rollout_img")
     R = a_env.cfg.obs_rows
     obs = torch.empty((K, B, R, 8), device="cuda")
     rew = torch.empty((K, B), device="cuda")

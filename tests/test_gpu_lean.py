@@ -57,7 +57,7 @@ def test_lean_staggered_equals_policy_plus_step(B, kw, kind, K, L):
     """Staggered episodes (1/L of the envs end at every step; some waves have more enders
     in a step than the prefetch covers, so both restart paths run), actions written."""
     a_env, b_env = _staggered_pair(B, L, kw)
-    assert a_env.rollout_kernel(K) == "k_rollout_lean"
+    assert a_env.rollout_kernel(K).startswith("k_rollout_lean")
     R = a_env.cfg.obs_rows
     obs = torch.empty((K, B, R, 8), device="cuda")
     rew = torch.empty((K, B), device="cuda")
@@ -83,7 +83,7 @@ def test_lean_lockstep_equals_policy_plus_step(kw, kind):
     no actions_out (the kernel variant that writes none)."""
     B, K = 131072, 20
     a_env, b_env = _staggered_pair(B, K, kw, stagger=False)
-    assert a_env.rollout_kernel(K) == "k_rollout_lean"
+    assert a_env.rollout_kernel(K).startswith("k_rollout_lean")
     R = a_env.cfg.obs_rows
     obs = torch.empty((K, B, R, 8), device="cuda")
     rew = torch.empty((K, B), device="cuda")
@@ -105,7 +105,7 @@ def test_lean_headline_size_equals_single_steps():
     -- obs, reward, done, terminal obs, episode-stats rows, the state afterwards."""
     B, K, L = 1 << 20, 20, 100
     a_env, b_env = _staggered_pair(B, L, {}, seed=11)
-    assert a_env.rollout_kernel(K) == "k_rollout_lean"
+    assert a_env.rollout_kernel(K).startswith("k_rollout_lean")
     R = a_env.cfg.obs_rows
     obs = torch.empty((K, B, R, 8), device="cuda")
     rew = torch.empty((K, B), device="cuda")
@@ -133,7 +133,7 @@ def test_lean_not_chosen_outside_its_shapes():
     assert LBVecEnv(131072, seed=1, as_tensors=True, episode_length=10).rollout_kernel(20) == "k_rollout_tpe"
     env = LBVecEnv(131072, seed=1, as_tensors=True)
     assert env.rollout_kernel(20, outputs_all=False) == "k_rollout_img"
-    assert env.rollout_kernel(20) == "k_rollout_lean"
+    assert env.rollout_kernel(20) == "k_rollout_lean_split"
 
 
 def test_rollout_past_4gib_takes_64bit_kernel():
@@ -174,7 +174,7 @@ def test_lean_shard_equals_slice_of_whole():
     n, K, L = 131072, 20, 20
     whole = LBVecEnv(2 * n, seed=3, as_tensors=True, episode_length=L)
     shard = LBVecEnv(n, seed=3, env_id_offset=n, as_tensors=True, episode_length=L)
-    assert whole.rollout_kernel(K) == "k_rollout_lean" and shard.rollout_kernel(K) == "k_rollout_lean"
+    assert whole.rollout_kernel(K) == "k_rollout_lean_split" and shard.rollout_kernel(K) == "k_rollout_lean_split"
     outs = []
     for e, B in ((whole, 2 * n), (shard, n)):
         e.reset()

@@ -45,7 +45,7 @@ def test_lean_rollout_equals_oracle(oracle_mod, B, cfg, K, kind):
     env = LBVecEnv(B, seed=seed, as_tensors=True, **kw)
     orc = oracle_mod.OracleBatch(kw, B, trace=False, seed=seed)
     orc.init()
-    assert env.rollout_kernel(K) == "k_rollout_lean"
+    assert env.rollout_kernel(K).startswith("k_rollout_lean")
     np.testing.assert_array_equal(env.reset().cpu().numpy(), orc.reset())
     gid = np.arange(B)
     for r in range(1, L):  # bench.py's stagger, both sides under their own random policy

@@ -144,19 +144,20 @@ def _rollout_kernel(B, steps, outputs_all=True, **kw):
 def test_rollout_kernel_choice():
     """lb_rollout_kernel (host only): the bench's launch takes k_rollout_lean; shapes it does
     not cover fall back to k_rollout_img / k_rollout_tpe / the slice kernel."""
-    assert _rollout_kernel(1 << 20, 20) == "k_rollout_lean"                       # the driver's launch
+    assert _rollout_kernel(1 << 20, 20) == "k_rollout_lean_split"                 # the driver's launch
     assert _rollout_kernel(1 << 20, 100) == "k_rollout_lean"
     assert _rollout_kernel(2000 * 64, 100, num_endpoints=6, num_nodes=48, num_zones=12) == "k_rollout_lean"
     assert _rollout_kernel(1 << 20, 20, outputs_all=False) == "k_rollout_img"     # an output not written
     assert _rollout_kernel((1 << 20) + 1, 20) == "k_rollout_img"                  # a partial last wave
     assert _rollout_kernel(40000, 20, geometry="tpe") == "k_rollout_img"          # 64-thread blocks
     assert _rollout_kernel(1 << 20, 20, num_endpoints=7) == "k_rollout_img"       # E without a lean build
-    assert _rollout_kernel(1 << 20, 20, reward_function="multi") == "k_rollout_lean"
+    assert _rollout_kernel(1 << 20, 20, reward_function="multi") == "k_rollout_lean_split"
+    assert _rollout_kernel(1 << 20, 32) == "k_rollout_lean_split" and _rollout_kernel(1 << 20, 33) == "k_rollout_lean"
     assert _rollout_kernel(1 << 20, 120) == "k_rollout_tpe"                       # K > L: in-loop resets
     assert _rollout_kernel(1 << 20, 20, auto_reset=False) == "k_rollout_tpe"
     assert _rollout_kernel(1 << 20, 20, num_nodes=100) == "policy+step launches"
     assert _rollout_kernel(4096, 20) == "k_rollout_slice"
-    assert _rollout_kernel(65536 + 320, 20, num_endpoints=6) == "k_rollout_lean"  # E = 6, N = 24: one zone word
+    assert _rollout_kernel(65536 + 320, 20, num_endpoints=6) == "k_rollout_lean_split"  # E = 6, N = 24: one zone word
     # lb_rollout's own preconditions hold here too: trace mode has no rollout kernel
     from lbk8s import LBConfig, _native
     c = LBConfig().to_c(trace=True)
@@ -180,7 +181,7 @@ def test_rollout_32bit_offsets_guard():
         assert L.lb_state_bytes(C.byref(c), mid, C.byref(n)) == 0
         fits = n.value <= 0xFFFFFFFF and mid * 9 * 32 <= 0xFFFFFFFF and mid * 16 * 8 <= 0xFFFFFFFF
         lo, hi = (mid, hi) if fits else (lo, mid)
-    assert _rollout_kernel(lo, 20) == "k_rollout_lean"
+    assert _rollout_kernel(lo, 20) == "k_rollout_lean_split"
     big = lo + 64 * 4096
     assert _rollout_kernel(big, 20) == "k_rollout_tpe"
     assert _rollout_kernel(1 << 24, 20) == "k_rollout_tpe"       # 2^24 envs: ~6.6 GB of state

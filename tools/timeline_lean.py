@@ -38,7 +38,7 @@ def main():
     L.lbx_set_timeline.argtypes = [C.c_void_p]
     B, K = args.envs, args.steps
     env = LBVecEnv(B, seed=0, as_tensors=True)
-    assert env.rollout_kernel(K) == "k_rollout_lean"
+    assert env.rollout_kernel(K).startswith("k_rollout_lean")
     R, EL = env.cfg.obs_rows, env.cfg.episode_length
     T = 100
     obs = torch.empty((T, B, R, 8), dtype=torch.float32, device="cuda")
