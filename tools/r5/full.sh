@@ -11,5 +11,3 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -3 gpurun_out/smoke_${TAG}.log
 timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_${TAG}.log 2>&1 || { tail -20 gpurun_out/bench_${TAG}.log; exit 1; }
 tail -1 gpurun_out/bench_${TAG}.log | cut -c1-400
-# diagnostic: the f64 log priced (a float-log build, wrong bits, timing only)
-bash tools/r5/ab_libs.sh r05_ab_cheaplog.jsonl "131072 1048576" 20 exp/liblbk8s_cur.so exp/liblbk8s_cheaplog.so
