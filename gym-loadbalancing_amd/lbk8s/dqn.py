@@ -36,6 +36,9 @@ from . import dist as lbdist
 from .deepsets import DQNDeepSetAgent, HUGE_NEG, allreduce_gradients
 
 
+DQN_STEPS_MAX = 32  # lb_dqn_steps' longest launch (include/lbk8s.h)
+
+
 def linear_schedule(start_e: float, end_e: float, duration: float, t: int) -> float:
     slope = (end_e - start_e) / duration
     return max(slope * t + start_e, end_e)
@@ -289,7 +292,7 @@ class DQN_DeepSets:
         """n vector steps from `parity`: one lb_dqn_steps launch where the env's shape has the
         one-launch step (the Q network is fixed within a period), else n _vector_step_dev."""
         env, pp = self.env, self.rb.pos_pp.data_ptr()
-        if n > 1 and self.multi_step and env.dqn_steps_supported(obs.shape[1]):
+        if 1 < n <= DQN_STEPS_MAX and self.multi_step and env.dqn_steps_supported(obs.shape[1]):
             end = parity ^ (n & 1)
             ex = self._ex[parity] if end != parity else self._ex_same[parity]
             env.dqn_steps(n, self._qfrag, obs, masks, ex, self._act, self._next_obs, self._rew, self._done_u8,
