@@ -78,6 +78,15 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_dqn_step(DSParams d, Params e, 
     const int s = lane >> 4, l16 = lane & 15;
     for (int64_t gi = wave; gi < groups; gi += nwaves) {
         const int64_t env0 = gi * P;
+        // the env held in registers across the launch's steps (as k_rollout_slice): loaded and
+        // observed once, its history counters and scalars stored after the last step
+        const int64_t env = env0 + s;
+        const bool live = s < P && env < e.B;
+        SEnv<1> v;
+        if (live) {
+            slice_load<16, 1>(e, env, l16, v);
+            slice_observe<1>(e, v);
+        }
         for (int i = 0; i < nsteps; ++i) {
             const bool explore = (exm >> i) & 1u;
             const int64_t ps = (pos + i) % r.slots;
@@ -89,17 +98,21 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_dqn_step(DSParams d, Params e, 
                 act = ds_group_actor<1, P, 2>(d, W, lane, env0, col, grp, R, h0, m0);
             }
             const int32_t ag = __shfl(act, s < P ? s : 0);
-            // the env step: lanes 16 s .. 16 s + 15 step env env0 + s (k_step_slice<16, 1>'s body)
-            const int64_t env = env0 + s;
+            // the env step: lanes 16 s .. 16 s + 15 step env env0 + s (k_step_slice<16, 1>'s body,
+            // the observed values kept in registers: a step changes the selected endpoint's)
             int a = 0;
-            if (s < P && env < e.B) {
-                SEnv<1> v;
-                slice_load<16, 1>(e, env, l16, v);
+            if (live) {
                 a = explore ? random_action(e, env, v.acc3, v.s.step) : ag;  // (exploring: :128-131)
                 if (explore && l16 == 0) d.actions[env] = a;
-                slice_step_body<16, 1, false, true, P == 4 ? NWB : 0>(e, env, l16, v, a, e.obs, e.reward, e.done,
-                                                                     e.rew64);
-                if (l16 == 0) slice_store_scalars<1>(e, env, v);
+                const SPrep pr = slice_prep<16, 1>(e, v, a);
+                bool done;
+                const double reward = slice_apply<16, 1, false, false>(e, env, l16, v, pr, done);
+                if (l16 == 0) {
+                    e.reward[env] = (float)reward;
+                    if (e.rew64) e.rew64[env] = reward;
+                    e.done[env] = (uint8_t)done;
+                }
+                slice_obs<16, 1, P == 4 ? NWB : 0>(e, env, l16, v, e.obs);
             }
             // the group's replay rows (lb_replay_add's), once the step's outputs have landed
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -121,8 +134,12 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_dqn_step(DSParams d, Params e, 
                     r.ep_cnt[env] += 1.0;
                 }
             }
-            // (step i + 1 reads the obs, the env state and the sums back)
+            // (step i + 1 reads the obs and the sums back)
             if (i + 1 < nsteps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (live) {
+            if (l16 < e.E) e.edyn[eidx(e, env, l16)] = v.ed[0];
+            if (l16 == 0) slice_store_scalars<1>(e, env, v);
         }
     }
     if (sync) {  // the last block to finish writes the device words (every block has read them)
