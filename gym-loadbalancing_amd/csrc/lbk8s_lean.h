@@ -54,6 +54,9 @@ constexpr int BUF_NT = 2;
 #ifndef LB_LEAN_MINW
 #define LB_LEAN_MINW 4
 #endif
+#ifndef LB_LEAN_XCD_MAP
+#define LB_LEAN_XCD_MAP 0
+#endif
 #ifdef LB_LEAN_NOGUARD
 #define LB_GUARD_S(...) ((void)0)
 #define LB_GUARD_V(...) ((void)0)
@@ -593,9 +596,16 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
     (void)NW;
     const LDims<ET, RT> d(p);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // block -> env group: blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
+    // workgroup dispatch); LB_LEAN_XCD_MAP gives each XCD a contiguous eighth of the groups
+#if LB_LEAN_XCD_MAP
+    const int64_t blk = gridDim.x % 8 == 0 ? (int64_t)(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8 : blockIdx.x;
+#else
+    const int64_t blk = blockIdx.x;
+#endif
     if constexpr (SPLIT) {
         if (wv == CW) {  // the copy wave (its block's env waves 0 .. CW - 1: envs blockIdx.x * 64 CW ..)
-            lean_copier<P, ACT, CW>(p, K, act_out, simg, sstage, (int64_t)blockIdx.x * 64 * CW);
+            lean_copier<P, ACT, CW>(p, K, act_out, simg, sstage, blk * 64 * CW);
             return;
         }
     }
@@ -604,7 +614,7 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
     // whole waves only (the host checks B % 64 == 0): every lane of a live wave is a live env,
     // and the waves past B in a partial last block leave (no block barrier follows: every
     // synchronisation below is within the wave; the split layout's blocks are whole)
-    const int64_t env0 = (int64_t)blockIdx.x * (SPLIT ? 64 * CW : NB) + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63);
+    const int64_t env0 = blk * (SPLIT ? 64 * CW : NB) + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63);
     if (env0 >= p.B) return;
 #ifdef LB_TIMELINE
     if (g_timeline && threadIdx.x % 64 == 0)
