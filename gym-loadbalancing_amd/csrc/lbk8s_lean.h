@@ -46,7 +46,10 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ Rsrc rsrc_of(const void* base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, -1, 0x00020000);
 }
-constexpr int BUF_NT = 2;
+#ifndef LB_LEAN_ST_AUX
+#define LB_LEAN_ST_AUX 2
+#endif
+constexpr int BUF_NT = LB_LEAN_ST_AUX;  // the output stores' cache policy (gfx940+: sc0 = 1, nt = 2, sc1 = 16)
 
 // Occupancy and hoisting guards of the step loop.  At 4 waves per SIMD (128 VGPRs) loop-invariant
 // values the compiler hoists out of the step loop spill, so they are laundered through empty asm
