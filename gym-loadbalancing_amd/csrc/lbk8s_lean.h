@@ -763,10 +763,18 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
         const int jn = jA < CMAX ? jA + 1 : CMAX;
         const int k0A = lem_k0(emA), c0A = em_c0(emA);
         // selected_endpoint_latency: lat0 on a first selection (LAT row 0 holds trunc(lat0))
+#ifdef LB_DIAG_NO_GATHER  // diagnostic build only (tools/r5): the step without its 4 table loads (wrong values)
+        r.sel_lat = 10.0 + jA + k0A;
+        r.sel_cpu = 20.0 + ed_m(edA) + c0A;
+        r.next_lat = 11.0 + jn + k0A;
+        r.next_cpu = 21.0 + Mn + c0A;
+        (void)l0off; (void)l0step; (void)cpu0;
+#else
         r.sel_lat = buf_ld_f64(blob, jA == 0 ? l0off + (uint32_t)ai * l0step : (uint32_t)(jA * LAT_ROWS + k0A) * 8u);
         r.sel_cpu = buf_ld_f64(blob, cpu0 + (uint32_t)(ed_m(edA) * CPU_ROWS + c0A) * 8u);
         r.next_lat = buf_ld_f64(blob, (uint32_t)(jn * LAT_ROWS + k0A) * 8u);
         r.next_cpu = buf_ld_f64(blob, cpu0 + (uint32_t)(Mn * CPU_ROWS + c0A) * 8u);
+#endif
 #ifndef LB_LEAN_NO_PREF
         fetch_next(step);
 #endif
@@ -841,7 +849,11 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
             // else loaded here: a block of its own, so the wait for the prefetched record stays
             // a counted vmcnt instead of a vmcnt(0) behind the stores above), the restarts in place
             const int pc = lane % P;
+#ifdef LB_LEAN_NO_PREF  // (diagnostic build: no record prefetch, every restart loads its records here)
+            bool pre = false;
+#else
             bool pre = __popcll(m) <= FAST;
+#endif
             for (uint64_t mm = m; mm;) {  // (wave-uniform)
                 uint64_t grp = mm;
 #pragma unroll
