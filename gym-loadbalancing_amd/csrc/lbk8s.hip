@@ -586,6 +586,14 @@ int lb_abi_version(void) { return LBK8S_ABI_VERSION; }
 #define LBK8S_SRC_HASH "unhashed"  // built outside the Makefile
 #endif
 const char* lb_source_hash(void) { return LBK8S_SRC_HASH; }
+#ifndef LBK8S_BUILD_FLAGS
+#define LBK8S_BUILD_FLAGS "unknown"  // built outside the Makefile
+#endif
+#ifndef LBK8S_BUILD_COMPILER
+#define LBK8S_BUILD_COMPILER "unknown"
+#endif
+const char* lb_build_flags(void) { return LBK8S_BUILD_FLAGS; }
+const char* lb_build_compiler(void) { return LBK8S_BUILD_COMPILER; }
 
 #ifdef LB_EXPERIMENTS
 int lbx_set_rollout_variant(int v) { g_rollout_variant = v; return 0; }
@@ -1012,11 +1020,12 @@ int lb_dqn_act(const float* frag, const float* obs, int64_t num_envs, int32_t nu
 
 namespace {
 // lb_dqn_step's one-launch shape: the env in the slice layout with 16 lanes per env (E <= 16
-// below 32,768 envs), R <= 16, at least four envs per SIMD
+// below 32,768 envs) and R <= 16.  A property of the shape only (not of the device's CU count):
+// the kernel is correct for any number of envs, and the learner's path must not change with the
+// part it runs on
 bool dqn_step_fusable(const lb_config* cfg, int64_t num_envs, int32_t num_elements) {
     const Geo g = geometry(cfg, num_envs);
-    const int64_t simds = (int64_t)device_cus() * 4;
-    return !g.tpe && g.W == 16 && g.EPL == 1 && num_elements <= 16 && (num_envs + DQN_P - 1) / DQN_P >= simds;
+    return !g.tpe && g.W == 16 && g.EPL == 1 && num_elements <= 16;
 }
 
 int dqn_steps_launch(const float* frag, float* obs, int64_t num_envs, int32_t num_elements, const uint8_t* masks,

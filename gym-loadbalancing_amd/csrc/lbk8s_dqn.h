@@ -4,21 +4,20 @@
 // the greedy action of the Q network's fused forward or every env's random action), lb_step
 // (the env step) and lb_replay_add (the replay write, obs <- next obs, the finished episodes'
 // sums).  Each env's chain -- its Q values, its action, its step, its replay row -- touches no
-// other env, so one wave carries it through for four envs at a time: the forward's P = 4 sets
-// of a wave iteration are exactly the four 16-lane env slices of the slice layout's step kernel
+// other env, so one wave carries it through for P envs at a time: the forward's P sets of a
+// wave iteration are exactly P 16-lane env slices of the slice layout's step kernel
 // (W = 16, one endpoint per lane: the env layout of E <= 16 at fewer than 32,768 envs).  At
 // config 5 (4096 envs) the step and replay kernels were ~5 us each of mostly launch ramp and
 // tail (profiles/r03_dqn_kernel_stats_setgrads.csv); here they follow the forward inside the
 // same waves.  Same functions, same order per env: bit for bit the three launches
-// (tests/test_gpu_dqn_step.py).
+// (tests/test_gpu_dqn_step.py).  The launch takes P = LB_DQN_P (2) envs per wave iteration
+// (lbk8s.hip: dqn_steps_launch); P = 4 is the other instantiation.
 #pragma once
 
 #include "lbk8s_deepsets.h"
 #include "lbk8s_slice.h"
 
 namespace lbk {
-
-constexpr int DQN_P = 4;  // envs per wave iteration (the Q forward's P, the slice step's envs per wave)
 
 struct DQNReplay {  // lb_replay_add's buffers
     int64_t slots;
@@ -41,12 +40,14 @@ struct DQNReplay {  // lb_replay_add's buffers
 //
 // nsteps > 1 (lb_dqn_steps): that many vector steps in the one launch.  Within a DQN train
 // period the Q network is fixed (the train step follows the period's last vector step) and
-// every env's chain touches no other env, so each wave takes its four envs through all the
+// every env's chain touches no other env, so each wave takes its P envs through all the
 // steps: step i explores by dqn_explores(t + i) (the same draw for every env), writes replay
 // slot pos + i, and leaves obs <- next obs and the env state for step i + 1, which the same
 // wave reads back after an s_waitcnt vmcnt(0).  The device words (vstep, pos, explore flag)
 // are then written by the launch's last block (sync: a counter the launch leaves at 0), after
-// every block has read them: in and out may be the same words.
+// every block has read them: in and out may be the same words.  The counter wraps itself: the
+// last block's atomicInc (limit gridDim.x - 1) returns gridDim.x - 1 and stores 0, so a launch
+// that starts with *sync == 0 leaves it 0 with no separate store.
 template <int P>
 __global__ __launch_bounds__(DS_BLOCK, 2) void k_dqn_step(DSParams d, Params e, DQNReplay r, int nsteps,
                                                          int32_t* sync) {
@@ -147,14 +148,13 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_dqn_step(DSParams d, Params e, 
         __syncthreads();
         if (threadIdx.x == 0) {
             __threadfence();
-            last = atomicAdd(sync, 1) == (int)gridDim.x - 1;
+            last = atomicInc(reinterpret_cast<unsigned*>(sync), gridDim.x - 1u) == gridDim.x - 1u;
         }
         __syncthreads();
         if (last && threadIdx.x == 0) {
             *d.ex.explore_out = (int32_t)((exm >> (nsteps - 1)) & 1u);
             *d.ex.vstep_out = t + nsteps;
             *r.pos_out = (pos + nsteps) % r.slots;
-            *sync = 0;
         }
     }
 }

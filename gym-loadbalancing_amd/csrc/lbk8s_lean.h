@@ -531,11 +531,45 @@ constexpr int LEAN_NB = LB_LEAN_NB;
 // env wave computes.  (The env work alone runs 26-30 us per step at 2^20 envs, the store stream
 // alone 46-55, the two in one wave 63-66; split, the env waves are half as many per SIMD, and
 // the 20-step launch gains 3-4%, the 100-step one loses 1-2%: profiles/r05_ab_split.jsonl.)
-template <int P, bool ACT, int CW>
+#ifndef LB_SPLIT_DRAWS
+#define LB_SPLIT_DRAWS 0
+#endif
+// the split layout's draw buffers (after the reward / done / action words in sstage): per step
+// parity b, 64 x1 and 64 x2 (f64) and 64 words a | r << 8 | n << 16 (byte offsets from sstage)
+constexpr uint32_t SD_BASE = 3 * 64 * 4, SD_BUF = 64 * 20, SD_X2 = 64 * 8, SD_W = 64 * 16;
+__device__ __forceinline__ double* sd_x1(uint32_t* sst, int b) {
+    return reinterpret_cast<double*>(reinterpret_cast<char*>(sst) + SD_BASE + b * SD_BUF);
+}
+__device__ __forceinline__ double* sd_x2(uint32_t* sst, int b) { return sd_x1(sst, b) + 64; }
+__device__ __forceinline__ uint32_t* sd_w(uint32_t* sst, int b) {
+    return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(sst) + SD_BASE + b * SD_BUF + SD_W);
+}
+// the draws of one env's next step (prep's, lbk8s_lean.h): the random policy's action at slot
+// cs, the request's X and I blocks at slot cs + 1 of episode ep -> the draw buffer
+template <int KIND>
+__device__ __forceinline__ void split_draws(const Params& p, int64_t env, uint32_t ep, uint32_t cs, uint32_t* sst,
+                                            int b, int lane) {
+    uint32_t a = 0;
+    if constexpr (KIND == LB_POLICY_RANDOM) a = bounded(draw_o(p, env, ep, cs, D_ACT).x, (uint32_t)p.A);
+    U4 wx, wi;
+    draw2_o(p, env, ep, cs + 1, D_REQ_X, D_REQ_I, wx, wi);
+    sd_x1(sst, b)[lane] = p.inv_rate * std_exp(wx.x, wx.y);
+    sd_x2(sst, b)[lane] = p.call * std_exp(wx.z, wx.w);
+    sd_w(sst, b)[lane] = a | (bounded(wi.x, 7) << 8) | (bounded(wi.y, (uint32_t)p.N) << 16);
+}
+
+template <int P, bool ACT, int CW, int KIND>
 __device__ __forceinline__ void lean_copier(const Params& p, int K, int32_t* act_out, uint32_t (*simg)[64 * IMG_W],
-                                            const uint32_t* sst, int64_t env0) {
+                                            uint32_t* sst, int64_t env0) {
     const int lane = threadIdx.x & 63;
     const bool h = (lane & 1) != 0;
+    uint32_t cs = 0, cep = 0;  // (LB_SPLIT_DRAWS) the env's step count and episode before the next step
+#ifndef LB_SPLIT_CPRIO
+#define LB_SPLIT_CPRIO -1
+#endif
+#if LB_SPLIT_CPRIO >= 0
+    __builtin_amdgcn_s_setprio(LB_SPLIT_CPRIO);
+#endif
     // the next episodes of the block's envs that end inside the launch, into their records (the
     // env wave's prologue in the single-wave layout; here beside the env wave's state loads and
     // image): 8 lanes per record, 8 records per pass, then barrier P
@@ -543,6 +577,8 @@ __device__ __forceinline__ void lean_copier(const Params& p, int K, int32_t* act
     for (int c = 0; c < CW; ++c) {
         const int64_t env = env0 + 64 * c + lane;
         const uint64_t sc = p.sc[env], acc3 = p.acc3[env];
+        cs = (uint32_t)(sc & 0xFFFF);
+        cep = (uint32_t)(acc3 >> 32);
         const int to_done = p.L - (int)(sc & 0xFFFF);
         uint64_t mm = __ballot(to_done >= 1 && to_done <= K);
         const uint32_t epi = (uint32_t)(acc3 >> 32) + 1;
@@ -555,9 +591,22 @@ __device__ __forceinline__ void lean_copier(const Params& p, int K, int32_t* act
             for (int j = 0; j < 8; ++j) mm &= mm - 1;
         }
     }
+#if LB_SPLIT_DRAWS
+    split_draws<KIND>(p, env0 + lane, cep, cs, sst, 0, lane);  // step 0's
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the records are written before P)
     block_lds_sync();  // P
     for (int k = 0; k < K; ++k) {
+#if LB_SPLIT_DRAWS
+        // the env after step k (an env ends at most once in the launch, L >= K: restart at L),
+        // then step k + 1's draws into buffer (k + 1) & 1 (its last reader, the env wave's
+        // preparation of step k - 1, finished before barrier B of step k - 2 / the prologue)
+        if (++cs == (uint32_t)p.L) {
+            cs = 0;
+            ++cep;
+        }
+        if (k + 1 < K) split_draws<KIND>(p, env0 + lane, cep, cs, sst, (k + 1) & 1, lane);
+#endif
         block_lds_sync();  // A: step k's images and words are in LDS
         float4 v[CW][P];
         uint32_t rw[CW], dn[CW], ac[CW];
@@ -593,6 +642,9 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
                                           uint32_t* sstage) {
     static_assert(CW == 0 || CW == 1, "one env wave per copy wave (two: the copy wave's registers for both blocks spilled)");
     constexpr bool SPLIT = CW > 0;
+#ifndef LB_SPLIT_ENVPRIO
+#define LB_SPLIT_ENVPRIO 1
+#endif
     constexpr int NB = SPLIT ? 64 * (CW + 1) : LEAN_NB, NW = SPLIT ? CW : NB / 64, P = 2 * RT, GT = 64 / P;
     constexpr int FAST = GT < REC_FETCH_MAX ? GT : REC_FETCH_MAX;  // restarts per step of the fast path
     static_assert(ET >= 1 && ET <= TPE_E && (RT == ET || RT == ET + 1), "compile-time geometry");
@@ -608,7 +660,7 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
 #endif
     if constexpr (SPLIT) {
         if (wv == CW) {  // the copy wave (its block's env waves 0 .. CW - 1: envs blockIdx.x * 64 CW ..)
-            lean_copier<P, ACT, CW>(p, K, act_out, simg, sstage, blk * 64 * CW);
+            lean_copier<P, ACT, CW, KIND>(p, K, act_out, simg, sstage, blk * 64 * CW);
             return;
         }
     }
@@ -741,7 +793,8 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
     };
 
     LPrepL pr;
-    auto prep = [&](auto&& between) {
+    auto prep = [&](const int j, auto&& between) {
+        (void)j;
         // the next step's action, its endpoint's 4 table gathers, the record prefetch, then the
         // request draws with the previous step's stores spread over between(0..5)
         LPrepL r;
@@ -752,7 +805,13 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
         tv.s.rz = (int)((v.s1 >> S1_RZ) & 3);
         const int step = (int)(v.s0 & 0xFFFF);
         tv.s.step = step;
+#if LB_SPLIT_DRAWS
+        // (split layout: the copy wave drew this step's action and request one step ahead)
+        const uint32_t dw = SPLIT ? sd_w(sstage, j & 1)[lane] : 0u;
+        const int a = SPLIT && KIND == LB_POLICY_RANDOM ? (int)(dw & 0xFFu) : lean_policy<KIND>(p, env, tv, em, ed);
+#else
         const int a = lean_policy<KIND>(p, env, tv, em, ed);
+#endif
         const bool accept = a < ET;
         const int ai = accept ? a : 0;
         const uint32_t emA = pick8(em, ai), edA = pick8(ed, ai);
@@ -784,24 +843,37 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
         asm volatile("" ::: "memory");
         between(0);
         asm volatile("" ::: "memory");
+        double x1, x2;
+        int rr, n;
+#if LB_SPLIT_DRAWS
+        if constexpr (SPLIT) {
+            x1 = sd_x1(sstage, j & 1)[lane];
+            x2 = sd_x2(sstage, j & 1)[lane];
+            rr = (int)((dw >> 8) & 0xFFu);
+            n = (int)(dw >> 16);
+        } else
+#endif
+        {
         const uint32_t episode = (uint32_t)(v.acc3 >> 32), slot = (uint32_t)(step + 1);
         U4 wx, wi;
         draw2_o(p, env, episode, slot, D_REQ_X, D_REQ_I, wx, wi);
         asm volatile("" ::"v"(wx.x), "v"(wx.y), "v"(wx.z), "v"(wx.w), "v"(wi.x), "v"(wi.y) : "memory");
         between(1);
         asm volatile("" ::: "memory");
-        const double x1 = p.inv_rate * std_exp(wx.x, wx.y);
+        x1 = p.inv_rate * std_exp(wx.x, wx.y);
         asm volatile("" ::"v"(x1) : "memory");
         between(2);
         asm volatile("" ::: "memory");
-        const double x2 = p.call * std_exp(wx.z, wx.w);
+        x2 = p.call * std_exp(wx.z, wx.w);
+        rr = (int)bounded(wi.x, 7);
+        n = (int)bounded(wi.y, (uint32_t)p.N);
+        }
         // next_request()'s clock (:1135-1139): the same operations as at the step
         r.arr = v.t + x1;
         r.dt = (float)((r.arr + x2) - r.arr);
         asm volatile("" ::"v"(r.arr), "v"(r.dt) : "memory");
         between(3);
         asm volatile("" ::: "memory");
-        const int rr = (int)bounded(wi.x, 7), n = (int)bounded(wi.y, (uint32_t)p.N);
         const uint64_t word = (NZW > 1 && n >= 32) ? v.nz1 : v.nz0;
         const uint32_t rz = (uint32_t)((word >> (2 * (n & 31))) & 3);
         r.arz = (uint32_t)a | ((uint32_t)((rr + 6) % 7) << 8) | (rz << 12) | ((uint32_t)oA << 14) |
@@ -814,7 +886,7 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
         return r;
     };
     if constexpr (SPLIT) block_lds_sync();  // P: the copy wave's records are written (the prefetch below reads them)
-    pr = prep([](int) {});
+    pr = prep(0, [](int) {});
     // (its loads land here, before the loop: pending at the loop header, they made every
     // wait for the preparation's values inside the loop a vmcnt(0) or close to it)
     asm volatile("" : "+v"(pr.sel_lat), "+v"(pr.sel_cpu), "+v"(pr.next_lat), "+v"(pr.next_cpu), "+v"(qn.x), "+v"(qn.y),
@@ -824,6 +896,9 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
     auto iter = [&](const int k) {
         LB_LTL(k, 0);
         // issue priority by progress (k_rollout_img): a wave behind the others goes first
+#if LB_SPLIT_ENVPRIO == 0
+        if (!SPLIT)
+#endif
 #ifndef LB_LEAN_NOPRIO
         {
             const int pl = 3 - (4 * k) / K;
@@ -839,7 +914,18 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
         const double reward = lean_apply_l<ET, RT, NAIVE ? (int)LB_REWARD_NAIVE : -1>(p, pr, v, em, ed, me);
         const uint64_t m = __ballot(done);
         LB_LTL(k, 1);
+#ifdef LB_DIAG_MIN_RESET  // diagnostic (wrong values): the restart's register part only, no image / record work
+        if (done) {
+            v.acc3 = (uint64_t)((uint32_t)(v.acc3 >> 32) + 1) << 32;
+            v.acc2 = 0; v.sum_lat = 0; v.sum_cpu = 0; v.sum_hi = 0; v.total = 0.0; v.s0 = 0;
+#pragma unroll
+            for (int i = 0; i < TPE_E; ++i) ed[i] = 0u;
+            new_episode = true;
+        }
+        if (false) {
+#else
         if (m) {  // VecEnv auto-reset: episode stats + terminal obs, then the record's episode
+#endif
             // (the stores below are younger than the prefetched record, so waiting for it does
             // not wait for them; the next gathers do, but a few 16-byte stores issued just
             // before them cost about nothing next to the gathers' own round trip)
@@ -899,13 +985,36 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
             sstage[192 * wv + lane] = __float_as_uint((float)reward);
             sstage[192 * wv + 64 + lane] = done ? 1u : 0u;
             if (ACT) sstage[192 * wv + 128 + lane] = (uint32_t)a_k;
+#ifndef LB_SPLIT_ORDER
+#define LB_SPLIT_ORDER 0
+#endif
+#if LB_SPLIT_ORDER == 0
             block_lds_sync();  // A
+            LB_LTL(k, 3);
             if (k + 1 < K) {
-                pr = prep([](int) {});
+                pr = prep(k + 1, [](int) {});
                 asm volatile("" : "+v"(pr.sel_lat), "+v"(pr.sel_cpu), "+v"(pr.next_lat), "+v"(pr.next_cpu),
                              "+v"(qn.x), "+v"(qn.y), "+v"(qn.z), "+v"(qn.w));
             }
+            LB_LTL(k, 4);
             block_lds_sync();  // B (the image and words are read)
+            LB_LTL(k, 5);
+#elif LB_SPLIT_ORDER == 1
+            if (k + 1 < K) {
+                pr = prep(k + 1, [](int) {});
+                asm volatile("" : "+v"(pr.sel_lat), "+v"(pr.sel_cpu), "+v"(pr.next_lat), "+v"(pr.next_cpu),
+                             "+v"(qn.x), "+v"(qn.y), "+v"(qn.z), "+v"(qn.w));
+            }
+            block_lds_sync();  // A
+            block_lds_sync();  // B (the image and words are read)
+#else
+            if (k + 1 < K) pr = prep(k + 1, [](int) {});
+            block_lds_sync();  // A
+            block_lds_sync();  // B (the image and words are read)
+            if (k + 1 < K)
+                asm volatile("" : "+v"(pr.sel_lat), "+v"(pr.sel_cpu), "+v"(pr.next_lat), "+v"(pr.next_cpu),
+                             "+v"(qn.x), "+v"(qn.y), "+v"(qn.z), "+v"(qn.w));
+#endif
             return;
         }
         // step k's outputs leave after step k + 1's gathers, spread over its request draws
@@ -938,7 +1047,7 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
             }
         };
         if (k + 1 < K) {
-            pr = prep(stores);
+            pr = prep(k + 1, stores);
             LB_LTL(k, 4);
             // the loads land here, behind the step's stores (a counted wait), and the values
             // the next step reads are this statement's, not the loads': none is pending at the
@@ -1036,7 +1145,8 @@ template <int KIND, int ET, int RT, int NZW, bool NAIVE, bool ACT, int CW>
 __global__ __launch_bounds__(64 * (CW + 1), LB_LEAN_SPLIT_LB) void k_rollout_lean_split(Params p, int K,
                                                                                        int32_t* act_out) {
     __shared__ __attribute__((aligned(16))) uint32_t simg[CW][64 * IMG_W];
-    __shared__ uint32_t sstage[CW * 3 * 64];  // each env wave's step reward, done, action words
+    // each env wave's step reward, done, action words; then (LB_SPLIT_DRAWS) the draw buffers
+    __shared__ __attribute__((aligned(16))) uint32_t sstage[CW * 3 * 64 + (LB_SPLIT_DRAWS ? 2 * SD_BUF / 4 : 0)];
     lean_body<KIND, ET, RT, NZW, NAIVE, ACT, CW>(p, K, act_out, simg, sstage);
 }
 

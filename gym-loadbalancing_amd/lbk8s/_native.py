@@ -15,7 +15,7 @@ CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
 # csrc/Makefile's SRCS, in order: the library embeds the SHA-256 of their concatenation
 SOURCES = ("lbk8s.hip", "lbk8s_common.h", "lbk8s_slice.h", "lbk8s_tpe.h", "lbk8s_rollout.h", "lbk8s_lean.h",
            "lbk8s_deepsets.h", "lbk8s_ds_train.h", "lbk8s_dqn.h", "../../include/lbk8s.h")
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 LB_REWARD = {"naive": 0, "latency": 1, "fairness": 2, "multi": 3}
 LB_RNG_PHILOX, LB_RNG_TRACE = 0, 1
@@ -93,6 +93,11 @@ class StaleNativeLibrary(RuntimeError):
     pass
 
 
+class NonDefaultBuild(StaleNativeLibrary):
+    """A product library compiled with other flags than csrc/Makefile's defaults (a -D knob of
+    a diagnostic build, another optimisation level): refused like a stale one."""
+
+
 class _Tolerant:
     """A diagnostic library of another ABI: symbols it lacks become no-op stand-ins, so
     setting their argtypes does not fail (calling one raises)."""
@@ -131,6 +136,33 @@ def source_hash():
         with open(path, "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]
+
+
+def _makefile_var(text, name):
+    """The default (`NAME ?= ...`, continuation lines joined) of a variable of csrc/Makefile."""
+    import re
+    m = re.search(r"^" + name + r" \?= (.*?)(?<!\\)$", text, re.S | re.M)
+    return " ".join(m.group(1).replace("\\\n", " ").split()) if m else ""
+
+
+def expected_build_flags():
+    """The flags csrc/Makefile compiles a product library with (HIPFLAGS with $(ARCH)
+    expanded, no DEFS), whitespace-normalised; None where the Makefile is absent."""
+    path = os.path.join(CSRC, "Makefile")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        text = fh.read()
+    flags = _makefile_var(text, "HIPFLAGS").replace("$(ARCH)", _makefile_var(text, "ARCH"))
+    return " ".join(flags.split())
+
+
+def build_hash(L):
+    """First 16 hex digits of SHA-256(source hash, flags, compiler) of a loaded library: one
+    word for the whole build (smoke prints it)."""
+    import hashlib
+    parts = [L.lb_source_hash(), L.lb_build_flags(), L.lb_build_compiler()]
+    return hashlib.sha256(b"\n".join(parts)).hexdigest()[:16]
 
 
 def lib():
@@ -196,11 +228,16 @@ def lib():
     if v != ABI_VERSION and product:
         raise RuntimeError(f"liblbk8s.so ABI {v} != expected {ABI_VERSION}; rebuild it")
     if product:  # (another LIB_PATH: a diagnostic build of other sources, tools/ only)
-        L.lb_source_hash.restype = C.c_char_p
+        for f in ("lb_source_hash", "lb_build_flags", "lb_build_compiler"):
+            getattr(L, f).restype = C.c_char_p
         built, now = L.lb_source_hash().decode(), source_hash()
         if now is not None and built != now:
             raise StaleNativeLibrary(f"{LIB_PATH} was built from sources {built}, the tree's are {now}: "
                                      "rebuild it (make -C gym-loadbalancing_amd/csrc, or __graft_entry__.build())")
+        flags, want = " ".join(L.lb_build_flags().decode().split()), expected_build_flags()
+        if want is not None and flags != want:
+            raise NonDefaultBuild(f"{LIB_PATH} was built with flags '{flags}', csrc/Makefile's defaults are "
+                                  f"'{want}': a diagnostic build is not the product (rebuild with make -B)")
     _lib = L
     return L
 
@@ -220,5 +257,6 @@ EXPORTED_SYMBOLS = ("lb_abi_version", "lb_last_error", "lb_validate_config", "lb
                     "lb_status", "lb_ds_pack", "lb_ds_forward", "lb_ds_train_forward",
                     "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax", "lb_replay_add", "lb_ppo_head",
                     "lb_episode_log", "lb_dqn_act", "lb_dqn_head", "lb_replay_sample", "lb_ds_set_grads",
-                    "lb_rollout_kernel", "lb_source_hash", "lb_reward64", "lb_dqn_step",
+                    "lb_rollout_kernel", "lb_source_hash", "lb_build_flags", "lb_build_compiler", "lb_reward64",
+                    "lb_dqn_step",
                     "lb_dqn_steps", "lb_dqn_steps_supported", "lb_ds_pack_pair", "lb_ds_forward_pair")

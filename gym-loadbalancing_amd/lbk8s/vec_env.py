@@ -491,6 +491,7 @@ class LBVecEnv:
         and the replay write (lb_replay_add into rb at the device slot *pos_in, obs <- next_obs,
         finished-episode sums) -- in one launch where the shape allows it (config 5's 4096 envs),
         else as those three launches; bit for bit the same either way."""
+        self._dqn_guard()
         R = obs.shape[1]
         _native.check(self._L.lb_dqn_step(
             frag.data_ptr(), obs.data_ptr(), self.num_envs, R, self._ptr(masks), self._ptr(self.state),
@@ -499,6 +500,16 @@ class LBVecEnv:
             rb.next_obs.data_ptr(), rb.actions.data_ptr(), rb.rewards.data_ptr(), rb.dones.data_ptr(),
             self._ptr(ep_sum), self._ptr(ep_cnt), self._stream()))
         return actions
+
+    def _dqn_guard(self):
+        """step_device's checks for the DQN step entry points (they step the env too).  A launch
+        captured into a HIP graph does not run: the learner captures its period graphs before
+        its reset(), and the replays follow the reset."""
+        if not self._reset_called and not self.torch.cuda.is_current_stream_capturing():
+            raise TypeError("step() called before reset()")
+        if self.trace_mode:
+            raise RuntimeError("the DQN step draws its exploration and actions from Philox; trace mode steps "
+                               "one call at a time (dqn_act + step)")
 
     def dqn_steps_supported(self, R):
         """Whether lb_dqn_steps (several DQN vector steps in one launch) covers this env with
@@ -510,6 +521,7 @@ class LBVecEnv:
         """lb_dqn_steps: n DQN vector steps (dqn_step n times, the explore draw, replay slot and
         step counter advancing per step) in one launch; pos_in / pos_out and the explore
         struct's step words may coincide.  sync: a device int32 tensor holding 0."""
+        self._dqn_guard()
         R = obs.shape[1]
         _native.check(self._L.lb_dqn_steps(
             frag.data_ptr(), obs.data_ptr(), self.num_envs, R, self._ptr(masks), self._ptr(self.state),

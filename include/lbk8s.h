@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LBK8S_ABI_VERSION 10
+#define LBK8S_ABI_VERSION 11
 
 /* reward_function names of loadbalancer_k8s_env.py:20-31 */
 enum { LB_REWARD_NAIVE = 0, LB_REWARD_LATENCY = 1, LB_REWARD_FAIRNESS = 2, LB_REWARD_MULTI = 3 };
@@ -142,6 +142,11 @@ const char* lb_last_error(void);
  * Makefile's SRCS, concatenated in order) it was compiled from; the host side refuses a
  * library whose sources have changed since (a stale build). */
 const char* lb_source_hash(void);
+/* (ABI 11) The rest of the build: the exact compiler flags, -D defines included (the Makefile's
+ * HIPFLAGS + DEFS), and the compiler's version.  The host side refuses a product library whose
+ * flags differ from the Makefile's defaults (a diagnostic "knob" build cannot pass for one). */
+const char* lb_build_flags(void);
+const char* lb_build_compiler(void);
 
 /* Validate a configuration (reference constructor constraints). 0 = ok. */
 int lb_validate_config(const lb_config* cfg);

@@ -12,8 +12,18 @@ for p in (REPO, PKG_DIR):
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
 
+def pytest_addoption(parser):
+    parser.addoption("--lib", default=None,
+                     help="run the tests against another build of liblbk8s.so (a diagnostic A/B build under "
+                          "exp/; the product tests load the in-tree library)")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+    lib = config.getoption("--lib")
+    if lib:
+        from lbk8s import _native
+        _native.LIB_PATH = os.path.abspath(lib)
 
 
 def golden_names(prefix=""):

@@ -37,11 +37,17 @@ def _ex(_native, st, parity, eps_start):
 
 
 @pytest.mark.parametrize("B,kw", [(4096, {}), (4096 + 8, dict(reward_function="multi", episode_length=9)),
-                                  (8192, dict(num_endpoints=6, reward_function="fairness", episode_length=7))])
+                                  (8192, dict(num_endpoints=6, reward_function="fairness", episode_length=7)),
+                                  (8, dict(num_endpoints=6, reward_function="multi", episode_length=7))])
 def test_dqn_step_equals_three_launches(B, kw):
+    """(8 envs: run.py's own DQN setup, far fewer envs than the chip's SIMDs: the one-launch
+    path is a property of the env's shape, not of the device's CU count.)"""
     kw = dict(dict(episode_length=7), **kw)
     a_env, frag, a_rb, a, nat = _setup(B, kw, seed=5)
     b_env, _, b_rb, b, _ = _setup(B, kw, seed=5)
+    # the path under test is the one-launch step (else lb_dqn_step would compare its fallback,
+    # the three launches, with themselves)
+    assert a_env.dqn_steps_supported(a_env.cfg.obs_rows)
     masks = torch.ones((B, a_env.cfg.obs_rows), dtype=torch.uint8, device="cuda")
     explored = greedy = 0
     for t in range(40):

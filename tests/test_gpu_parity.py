@@ -82,6 +82,13 @@ PHILOX_CFGS = {
     "e100_fair_norej": dict(num_endpoints=100, reward_function="fairness", rejection_allowed=False),
     "e3_latency_short": dict(num_endpoints=3, reward_function="latency", episode_length=9),
     "e13_n70": dict(num_endpoints=13, num_nodes=70, num_zones=7, reward_function="multi"),
+    # E in (100, 256]: the reference's own sweep lists 128 / 150 / 180 (run_baselines.py:32);
+    # 512 envs run the one-env-per-wave slice shape, W = 64 with EPL = 2 (E = 128) or 4 (E > 128)
+    "e128_multi": dict(num_endpoints=128, reward_function="multi"),
+    "e150_fair_norej": dict(num_endpoints=150, reward_function="fairness", rejection_allowed=False),
+    "e180_multi_n64": dict(num_endpoints=180, num_nodes=64, num_zones=6, reward_function="multi",
+                           latency_weight=0.5, cpu_weight=0.3, gini_weight=0.2),
+    "e256_latency_n200": dict(num_endpoints=256, num_nodes=200, num_zones=9, reward_function="latency"),
 }
 
 
@@ -142,6 +149,14 @@ MANY_CFGS = {
                           latency_weight=0.5, cpu_weight=0.3, gini_weight=0.2, episode_length=7),
     "e5_fair_norej_l10": dict(num_endpoints=5, num_nodes=70, reward_function="fairness",
                               rejection_allowed=False, episode_length=10),
+    # E in (100, 256] at 32,768 envs: W = 32 / EPL = 4 (E = 128) and W = 64 / EPL = 4 (E > 128)
+    "e128_fair_l10": dict(num_endpoints=128, reward_function="fairness", episode_length=10),
+    "e150_multi_norej_l10": dict(num_endpoints=150, reward_function="multi", rejection_allowed=False,
+                                 episode_length=10),
+    "e180_latency_n48_l10": dict(num_endpoints=180, num_nodes=48, num_zones=5, reward_function="latency",
+                                 episode_length=10),
+    "e256_multi_l10": dict(num_endpoints=256, reward_function="multi", latency_weight=1.0, cpu_weight=0.0,
+                           gini_weight=0.0, episode_length=10),
 }
 
 
