@@ -29,7 +29,7 @@
 #include "lbk8s_slice.h"
 #include "lbk8s_tpe.h"
 #include "lbk8s_rollout.h"
-#include "lbk8s_lean.h"
+#include "lbk8s_lean_launch.h"
 
 namespace lbk {
 
@@ -531,25 +531,6 @@ int device_cus() {
     return cus;
 }
 
-// k_rollout_lean: one 64-thread block per 64-env group (B % 64 == 0).  Launches of at most
-// LEAN_SPLIT_MAX_K steps pair each env wave with a copy wave in a 128-thread block
-// (k_rollout_lean_split, lbk8s_lean.h: lean_copier): 3-4% faster at K = 20 (131,072 and 2^20
-// envs), 1-2% slower at K = 100 (profiles/r05_ab_split.jsonl)
-#ifndef LB_LEAN_SPLIT_MAX_K
-#define LB_LEAN_SPLIT_MAX_K 32
-#endif
-constexpr int LEAN_SPLIT_MAX_K = LB_LEAN_SPLIT_MAX_K;
-template <int KIND, int ET, int RT, int NZW, bool NAIVE, bool ACT>
-void launch_lean(const Params& p, int64_t B, int steps, int32_t* act, hipStream_t s) {
-    if (steps <= LEAN_SPLIT_MAX_K) {
-        hipLaunchKernelGGL((k_rollout_lean_split<KIND, ET, RT, NZW, NAIVE, ACT, 1>), dim3((unsigned)(B / 64)), dim3(128), 0,
-                           s, p, steps, act);
-        return;
-    }
-    hipLaunchKernelGGL((k_rollout_lean<KIND, ET, RT, NZW, NAIVE, ACT>), dim3((unsigned)((B + LEAN_NB - 1) / LEAN_NB)),
-                       dim3(LEAN_NB), 0, s, p, steps, act);
-}
-
 // Which kernel lb_rollout launches (lb_rollout_kernel reports it, LB_ROLLOUT_*).
 // Per-lane addresses of the thread-per-env rollouts are 32-bit byte offsets from scalar bases
 // (k_rollout_img: the state blob and the ep_stats rows; k_rollout_lean also the obs slot and
@@ -582,24 +563,18 @@ extern "C" {
 
 int lb_abi_version(void) { return LBK8S_ABI_VERSION; }
 
-#ifndef LBK8S_SRC_HASH
-#define LBK8S_SRC_HASH "unhashed"  // built outside the Makefile
-#endif
-const char* lb_source_hash(void) { return LBK8S_SRC_HASH; }
-#ifndef LBK8S_BUILD_FLAGS
-#define LBK8S_BUILD_FLAGS "unknown"  // built outside the Makefile
-#endif
-#ifndef LBK8S_BUILD_COMPILER
-#define LBK8S_BUILD_COMPILER "unknown"
-#endif
-const char* lb_build_flags(void) { return LBK8S_BUILD_FLAGS; }
-const char* lb_build_compiler(void) { return LBK8S_BUILD_COMPILER; }
+// (lb_source_hash, lb_build_flags, lb_build_compiler: lbk8s_build.cpp, rebuilt with every source change)
 
 #ifdef LB_EXPERIMENTS
 int lbx_set_rollout_variant(int v) { g_rollout_variant = v; return 0; }
 #endif
 #ifdef LB_TIMELINE
-int lbx_set_timeline(uint64_t* buf) { return hipMemcpyToSymbol(HIP_SYMBOL(g_timeline), &buf, sizeof(buf)) == hipSuccess ? 0 : -1; }
+int lbx_set_timeline(uint64_t* buf) {  // k_rollout_img's (this unit) and k_rollout_lean's (one per policy unit)
+    int r = hipMemcpyToSymbol(HIP_SYMBOL(g_timeline), &buf, sizeof(buf)) == hipSuccess ? 0 : -1;
+    r |= lbx_set_timeline_lean_0(buf) | lbx_set_timeline_lean_1(buf) | lbx_set_timeline_lean_2(buf) |
+         lbx_set_timeline_lean_3(buf);
+    return r;
+}
 #endif
 
 const char* lb_last_error(void) { return g_err.c_str(); }

@@ -40,7 +40,7 @@
 namespace lbk {
 
 #ifdef LB_TIMELINE
-__device__ uint64_t* g_timeline;  // [waves][K + 2] s_memrealtime (100 MHz) stamps, or NULL
+static __device__ uint64_t* g_timeline;  // [waves][K + 2] s_memrealtime (100 MHz) stamps, or NULL
 #endif
 
 // lem (the rollout's emeta register): zone[0:2) owner[2:10) type[10:13) c0[13:20) k0[20:29)

@@ -14,7 +14,8 @@ _PRODUCT_LIB = LIB_PATH
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
 # csrc/Makefile's SRCS, in order: the library embeds the SHA-256 of their concatenation
 SOURCES = ("lbk8s.hip", "lbk8s_common.h", "lbk8s_slice.h", "lbk8s_tpe.h", "lbk8s_rollout.h", "lbk8s_lean.h",
-           "lbk8s_deepsets.h", "lbk8s_ds_train.h", "lbk8s_dqn.h", "../../include/lbk8s.h")
+           "lbk8s_deepsets.h", "lbk8s_ds_train.h", "lbk8s_dqn.h", "../../include/lbk8s.h", "lbk8s_lean_launch.h",
+           "lbk8s_lean_inst.hip", "lbk8s_build.cpp")
 ABI_VERSION = 11
 
 LB_REWARD = {"naive": 0, "latency": 1, "fairness": 2, "multi": 3}

@@ -124,7 +124,7 @@ def test_host_asan_ubsan_abi():
     import subprocess
     if shutil.which("make") is None or not os.path.exists("/opt/rocm/bin/hipcc"):
         pytest.skip("no hipcc / make")
-    r = subprocess.run(["make", "-s", "-C", os.path.join(REPO, "tests", "asan"), "run"], capture_output=True,
+    r = subprocess.run(["make", "-s", "-j6", "-C", os.path.join(REPO, "tests", "asan"), "run"], capture_output=True,
                        text=True, timeout=600)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     assert "abi_asan: ok" in r.stdout
