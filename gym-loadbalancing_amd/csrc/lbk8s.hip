@@ -870,7 +870,7 @@ int lb_ds_pack(const lb_ds_weights* w, float* frag_out, void* stream) {
     if (!w || !frag_out) return fail("weights/frag_out NULL");
     for (int i = 0; i < 3; ++i)
         if (!w->actor_lambda[i] || !w->actor_gamma[i]) return fail("actor weights are required");
-    hipLaunchKernelGGL(k_ds_pack, dim3((DS_FLOATS + 255) / 256), dim3(256), 0, (hipStream_t)stream, *w, frag_out);
+    hipLaunchKernelGGL(k_ds_pack, dim3((DS_IMG_FLOATS + 255) / 256), dim3(256), 0, (hipStream_t)stream, *w, frag_out);
     return check_launch();
 }
 
@@ -926,7 +926,7 @@ extern "C" {
 
 int lb_ds_forward(const float* frag, const float* obs, int64_t num_envs, int32_t num_elements, float* logits_out,
                   float* value_out, void* stream) {
-    static_assert(DS_FLOATS == LB_DS_FRAG_FLOATS, "fragment layout and header disagree");
+    static_assert(DS_IMG_FLOATS == LB_DS_FRAG_FLOATS, "weight image layout and header disagree");
     if (!frag || !obs || num_envs < 1) return fail("frag/obs NULL or num_envs < 1");
     if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS_FWD)
         return fail("num_elements must be in [1, 257] (LB_DS_MAX_ELEMENTS_FWD)");
@@ -1233,6 +1233,36 @@ int lb_ds_train_backward(const float* bwd_frag, const float* obs, int64_t num_en
     static_assert(DSW_SLOTS % (2 * DSR_GROUPS) == 0, "reduction stride");
     hipLaunchKernelGGL(k_ds_wgrad_reduce, dim3((2 * DSW_FLOATS + DSR_COLS - 1) / DSR_COLS), dim3(DSR_COLS * DSR_GROUPS),
                        0, s, workspace, wgrad_out, (int)actor, (int)critic);
+    return check_launch();
+}
+
+int lb_ds_over_sets(const lb_set_job* jobs, int32_t num_jobs, int64_t num_sets, float* workspace,
+                    int64_t workspace_floats, void* stream) {
+    if (!jobs || num_jobs < 1 || num_jobs > OS_JOBS || num_sets < 1 || !workspace)
+        return fail("lb_ds_over_sets: jobs NULL, num_jobs not in [1, 16], num_sets < 1 or workspace NULL");
+    OverSetsParams p{};
+    int tiles = 0, row = 0;
+    for (int i = 0; i < num_jobs; ++i) {
+        const lb_set_job& j = jobs[i];
+        if (!j.b || !j.out || j.M < 1 || j.N < 1 || j.M > 64 || j.N > 64 || (!j.a && j.M != 1))
+            return fail("lb_ds_over_sets: a job needs b and out, 1 <= M, N <= 64 (M == 1 when a is NULL)");
+        p.job[i] = OverSetsJob{j.a, j.lda, j.b, j.ldb, j.M, j.N, j.scale, j.out, row, tiles};
+        tiles += ((j.M + 15) / 16) * ((j.N + 15) / 16);
+        row += j.M * j.N;
+    }
+    p.njobs = num_jobs;
+    p.ntiles = tiles;
+    p.row = row;
+    p.S = num_sets;
+    p.work = workspace;
+    const int64_t spans = (num_sets + OS_SPAN - 1) / OS_SPAN;
+    if (spans * row > workspace_floats) return fail("lb_ds_over_sets: workspace too small (spans x outputs)");
+    if (spans > 65535) return fail("lb_ds_over_sets: num_sets too large");
+    hipLaunchKernelGGL(k_ds_over_sets, dim3((unsigned)((tiles + 3) / 4), (unsigned)spans), dim3(256), 0,
+                       (hipStream_t)stream, p);
+    if (int r = check_launch()) return r;
+    hipLaunchKernelGGL(k_ds_over_sets_reduce, dim3((unsigned)((row + 255) / 256)), dim3(256), 0, (hipStream_t)stream, p,
+                       (int)spans);
     return check_launch();
 }
 

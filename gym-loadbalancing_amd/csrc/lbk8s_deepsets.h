@@ -86,6 +86,71 @@ enum : int {
 constexpr int DS_BLOCK = 512;             // 8 waves: 2 per SIMD
 constexpr int DS_LDS_FLOATS = DS_FLOATS;  // 132 KiB of weight fragments: one block per CU
 
+// The VALU image (round 6), appended to the fragment image at DS_FLOATS, for the forwards with one
+// env per wave iteration and at least three 16-element set tiles (R in 33..80: config 4's R = 65).
+// There every matrix-VECTOR product of the networks -- each equivariant layer's Gamma term
+// (Gamma max_set(h), one vector per set), the critic's layer 3 on the set mean and max, rho --
+// filled one of the 16 columns of its MFMA tiles (64 MFMAs each, 33% of the forward's MFMA issue
+// at R = 65); here each is 64 lane-wise dot products on the VALU (lane f: output feature f) from
+// row-major weights, padded rows (stride 68 / 12 floats: a 16-lane ds_read_b128 group covers the
+// 64 banks once).  The set-wise Lambda terms stay on MFMA (their fragments are copied here so the
+// image is one contiguous LDS stage).  Gamma matrices are stored negated, as the fragments.
+enum : int {
+    VG_RS = 68, VG_RS8 = 12,
+    VG_A1L = 0, VG_A2L = 512, VG_A3L = 4608, VG_A3G = 5632, VG_A1G = 6656, VG_A2G = 7424, VG_ACTOR = 11776,
+    VG_C1L = 11776, VG_C2L = 12288, VG_C1G = 16384, VG_C2G = 17152, VG_C3L = 21504, VG_C3G = 25856,
+    VG_R1W = 30208, VG_R1B = 34560, VG_R2W = 34624, VG_R2B = 34688, VG_FLOATS = 34692,
+    DS_IMG_FLOATS = DS_FLOATS + VG_FLOATS,
+    VG_SCRATCH = 128,  // per wave: the matvec input x[64] and output y[64]
+};
+template <int TS, int P>
+struct DSGeom {
+    static constexpr bool VG = TS >= 3 && P == 1;
+    static constexpr int LDS = VG ? VG_FLOATS + (DS_BLOCK / 64) * VG_SCRATCH : DS_LDS_FLOATS;
+};
+// (wave-local LDS ordering: the wave's own writes before its later reads by other lanes)
+__device__ __forceinline__ void ds_wave_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// the set's max (P = 1: every lane holds it, feature in(k, grp)) into x[KS * 4]
+template <int KS>
+__device__ __forceinline__ void vg_put(const float (&mb)[KS], float* x, int col, int grp) {
+    if (col != 0) return;
+    if constexpr (KS == 2) {
+        x[grp] = mb[0];
+        x[4 + grp] = mb[1];
+    } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            *reinterpret_cast<float4*>(x + 16 * t + 4 * grp) = make_float4(mb[4 * t], mb[4 * t + 1], mb[4 * t + 2], mb[4 * t + 3]);
+    }
+}
+// acc + sum_j W[f][j] x[j] for this lane's output feature f = lane (ascending j)
+template <int KIN, int S>
+__device__ __forceinline__ float vg_dot(const float* Wrm, const float* x, int lane, float acc) {
+    const float* w = Wrm + lane * S;
+#pragma unroll
+    for (int j = 0; j < KIN; j += 4) {
+        const float4 a = *reinterpret_cast<const float4*>(w + j), b = *reinterpret_cast<const float4*>(x + j);
+        acc = fmaf(a.x, b.x, acc);
+        acc = fmaf(a.y, b.y, acc);
+        acc = fmaf(a.z, b.z, acc);
+        acc = fmaf(a.w, b.w, acc);
+    }
+    return acc;
+}
+// (-Gamma) max_set(h) by VALU into the accumulator layout: g[nt][i] = y[16 nt + 4 grp + i]
+template <int KS>
+__device__ __forceinline__ void vg_gamma(const float* Grm, const float (&mb)[KS], float* xs, int lane, dsf4 (&g)[4]) {
+    const int col = lane & 15, grp = lane >> 4;
+    vg_put<KS>(mb, xs, col, grp);
+    ds_wave_fence();
+    const float y = vg_dot<4 * KS, KS == 2 ? VG_RS8 : VG_RS>(Grm, xs, lane, 0.f);
+    xs[64 + lane] = y;
+    ds_wave_fence();
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) g[nt] = *reinterpret_cast<const dsf4*>(xs + 64 + 16 * nt + 4 * grp);
+    ds_wave_fence();  // (read before the scratch is rewritten)
+}
+
 __device__ __forceinline__ dsf4 mfma4(float a, float b, dsf4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -255,17 +320,25 @@ __device__ __forceinline__ void set_max_store(const float (&h)[P * TS][KS], floa
 // are independent (a dependent f32 MFMA waits 40 cycles against 32 for issue, and one chain
 // at a time left the DPP broadcast of each Gamma result on the critical path).  Every
 // element still accumulates Gamma first, then k = 0..KS-1 in order: the same bits.
-template <int TS, int P, int KS, int ACT>
+// VG (DSGeom<TS, P>::VG): G is the row-major Gamma of the VALU image and xs the wave's scratch;
+// the Gamma term is then vg_gamma's instead of 4 x KS MFMAs with one useful column
+template <int TS, int P, int KS, int ACT, bool VG = false>
 __device__ __forceinline__ void eq_layer(const float* L, const float* G, const float (&h)[P * TS][KS],
-                                         const float (&mb)[KS], float (&out)[P * TS][16], int lane) {
+                                         const float (&mb)[KS], float (&out)[P * TS][16], int lane,
+                                         float* xs = nullptr) {
     constexpr int ST = P * TS;
     dsf4 g[4];
+    if constexpr (VG) {
+        static_assert(P == 1, "one env per wave iteration");
+        vg_gamma<KS>(G, mb, xs, lane, g);
+    } else {
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) g[nt] = dsf4{0.f, 0.f, 0.f, 0.f};
+        for (int nt = 0; nt < 4; ++nt) g[nt] = dsf4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < KS; ++k)
+        for (int k = 0; k < KS; ++k)
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) g[nt] = mfma4(G[(nt * KS + k) * 64 + lane], mb[k], g[nt]);
+            for (int nt = 0; nt < 4; ++nt) g[nt] = mfma4(G[(nt * KS + k) * 64 + lane], mb[k], g[nt]);
+    }
     constexpr int NTB = ST <= 2 ? 4 : 1;  // output tiles per pass
 #pragma unroll
     for (int nt0 = 0; nt0 < 4; nt0 += NTB) {
@@ -354,27 +427,31 @@ __device__ __forceinline__ void ds_group_obs(const DSParams& p, int64_t env0, in
 
 // one wave iteration's P envs: the actor (or Q network) Eq(8->64) ReLU Eq(64->64) ELU Eq(64->1);
 // logits / training rows / the masked greedy action (ARGMAX: lane s < P returns env0 + s's)
+// (W: the fragment image, or the VALU image with xs the wave's scratch: DSGeom<TS, P>::VG)
 template <int TS, int P, int MODE>
 __device__ __forceinline__ int32_t ds_group_actor(const DSParams& p, const float* W, int lane, int64_t env0, int col,
-                                                  int grp, int R, const float (&h0)[P * TS][2], const float (&m0)[2]) {
-    constexpr bool TRAIN = MODE == 1, ARGMAX = MODE == 2;
+                                                  int grp, int R, const float (&h0)[P * TS][2], const float (&m0)[2],
+                                                  float* xs = nullptr) {
+    constexpr bool TRAIN = MODE == 1, ARGMAX = MODE == 2, VG = DSGeom<TS, P>::VG;
+    constexpr int A1L = VG ? VG_A1L : DS_A1L, A1G = VG ? VG_A1G : DS_A1G, A2L = VG ? VG_A2L : DS_A2L,
+                  A2G = VG ? VG_A2G : DS_A2G, A3L = VG ? VG_A3L : DS_A3L, A3G = VG ? VG_A3G : DS_A3G;
     int32_t act = -1;
     float h1[P * TS][16], m1[16], h2[P * TS][16], m2[16];
     // ---- actor: Eq(8->64) ReLU Eq(64->64) ELU Eq(64->1)
     if (p.actor) {
-        eq_layer<TS, P, 2, 1>(W + DS_A1L, W + DS_A1G, h0, m0, h1, lane);
+        eq_layer<TS, P, 2, 1, VG>(W + A1L, W + A1G, h0, m0, h1, lane, xs);
         if (TRAIN) store_rows<TS, P>(p.save_actor, h1, env0, p.B, R, col, grp);
         if (TRAIN) set_max_store<TS, P, 16>(h1, m1, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX1A, LB_DSV_ID1A);
         else set_max_batched<TS, P, 16>(h1, m1, col, R);
-        eq_layer<TS, P, 16, 2>(W + DS_A2L, W + DS_A2G, h1, m1, h2, lane);
+        eq_layer<TS, P, 16, 2, VG>(W + A2L, W + A2G, h1, m1, h2, lane, xs);
         if (TRAIN) store_rows<TS, P>(p.save_actor + p.B * (int64_t)R * 64, h2, env0, p.B, R, col, grp);
         if (TRAIN) set_max_store<TS, P, 16>(h2, m2, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX2A, LB_DSV_ID2A);
         else set_max_batched<TS, P, 16>(h2, m2, col, R);
         // layer 3 (64 -> 1) on the VALU: a 16-row output tile would use 1/16 of an MFMA.
         // Lane (col, grp) dots its 16 features with Lambda3 / -Gamma3 (row 0 of the
         // fragments: column 0 of its row group), then the 4 row groups are summed.
-        const float* L = W + DS_A3L + 16 * grp;
-        const float* G = W + DS_A3G + 16 * grp;
+        const float* L = W + A3L + 16 * grp;
+        const float* G = W + A3G + 16 * grp;
         float gl = 0.f;
 #pragma unroll
         for (int k = 0; k < 16; ++k) gl += G[k * 64] * m2[k];
@@ -432,13 +509,16 @@ __device__ __forceinline__ int32_t ds_group_actor(const DSParams& p, const float
 // its half of the grid), W the block's LDS weight region
 template <int TS, int P, int MODE>
 __device__ __forceinline__ void ds_fwd_body(const DSParams& p, float* W, int blk, int nblk) {
-    constexpr bool TRAIN = MODE == 1, ARGMAX = MODE == 2;
-    // stage the weight fragments (once per block; blocks are persistent); an actor-only
-    // launch (DQN) stages only the actor's
-    const int nstage = (ARGMAX || !p.critic) ? DS_C1L : DS_FLOATS;
+    constexpr bool TRAIN = MODE == 1, ARGMAX = MODE == 2, VG = DSGeom<TS, P>::VG;
+    // stage the weight image (once per block; blocks are persistent): the fragment image, or
+    // the VALU image (VG); an actor-only launch (DQN) stages only the actor's part
+    const int nstage = VG ? ((ARGMAX || !p.critic) ? (int)VG_ACTOR : (int)VG_FLOATS)
+                          : ((ARGMAX || !p.critic) ? (int)DS_C1L : (int)DS_FLOATS);
+    const float* src = p.wfrag + (VG ? DS_FLOATS : 0);
     for (int i = threadIdx.x * 4; i < nstage; i += DS_BLOCK * 4)
-        *reinterpret_cast<float4*>(W + i) = *reinterpret_cast<const float4*>(p.wfrag + i);
+        *reinterpret_cast<float4*>(W + i) = *reinterpret_cast<const float4*>(src + i);
     __syncthreads();
+    float* xs = VG ? W + VG_FLOATS + (threadIdx.x >> 6) * VG_SCRATCH : nullptr;
     const int lane = threadIdx.x & 63;
     // wave-major numbering: a batch of fewer groups than waves puts one wave on each SIMD
     // of every CU (waves 0-3 of a block sit on its 4 SIMDs) before any SIMD takes a second
@@ -451,16 +531,18 @@ __device__ __forceinline__ void ds_fwd_body(const DSParams& p, float* W, int blk
         const int64_t env0 = gi * P;
         float h0[P * TS][2], m0[2];
         ds_group_obs<TS, P, MODE>(p, env0, col, grp, R, h0, m0);
-        ds_group_actor<TS, P, MODE>(p, W, lane, env0, col, grp, R, h0, m0);
+        ds_group_actor<TS, P, MODE>(p, W, lane, env0, col, grp, R, h0, m0, xs);
         float h1[P * TS][16], m1[16], h2[P * TS][16], m2[16];
         if (ARGMAX || !p.critic) continue;
 
         // ---- critic: psi = Eq ELU Eq ELU Eq, mean over the set, rho = Linear ELU Linear
-        eq_layer<TS, P, 2, 2>(W + DS_C1L, W + DS_C1G, h0, m0, h1, lane);
+        constexpr int C1L = VG ? VG_C1L : DS_C1L, C1G = VG ? VG_C1G : DS_C1G, C2L = VG ? VG_C2L : DS_C2L,
+                      C2G = VG ? VG_C2G : DS_C2G;
+        eq_layer<TS, P, 2, 2, VG>(W + C1L, W + C1G, h0, m0, h1, lane, xs);
         if (TRAIN) store_rows<TS, P>(p.save_critic, h1, env0, p.B, R, col, grp);
         if (TRAIN) set_max_store<TS, P, 16>(h1, m1, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX1C, LB_DSV_ID1C);
         else set_max_batched<TS, P, 16>(h1, m1, col, R);
-        eq_layer<TS, P, 16, 2>(W + DS_C2L, W + DS_C2G, h1, m1, h2, lane);
+        eq_layer<TS, P, 16, 2, VG>(W + C2L, W + C2G, h1, m1, h2, lane, xs);
         if (TRAIN) store_rows<TS, P>(p.save_critic + p.B * (int64_t)R * 64, h2, env0, p.B, R, col, grp);
         if (TRAIN) set_max_store<TS, P, 16>(h2, m2, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX2C, LB_DSV_ID2C);
         else set_max_batched<TS, P, 16>(h2, m2, col, R);
@@ -468,6 +550,44 @@ __device__ __forceinline__ void ds_fwd_body(const DSParams& p, float* W, int blk
         // mean_r(Lambda3 c2[r] - Gamma3 max(c2)) = Lambda3 mean_r(c2) - Gamma3 max(c2): one
         // matrix-vector pair on the batched (column c = env c mod P) operands instead of a
         // 64x64 layer over every row
+        if constexpr (VG) {  // the pair, rho's two layers: lane f's dot products (xs: x, then y)
+            float sm[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                float v = 0.f;
+#pragma unroll
+                for (int t = 0; t < TS; ++t)
+                    if (16 * t + col < R) v += h2[t][k];
+                sm[k] = v;
+            }
+            row_reduce<false>(sm);
+            const float invR = 1.0f / (float)R;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) sm[k] *= invR;
+            vg_put<16>(m2, xs, col, grp);
+            ds_wave_fence();
+            float mean = vg_dot<64, VG_RS>(W + VG_C3G, xs, lane, 0.f);  // (-Gamma3) max, then Lambda3 mean
+            ds_wave_fence();
+            vg_put<16>(sm, xs, col, grp);
+            ds_wave_fence();
+            mean = vg_dot<64, VG_RS>(W + VG_C3L, xs, lane, mean);
+            if (TRAIN) {
+                if (env0 < p.B) p.psi_mean[env0 * 64 + lane] = mean;
+                ds_wave_fence();
+                continue;
+            }
+            ds_wave_fence();
+            xs[lane] = mean;
+            ds_wave_fence();
+            const float r1 = act_elu(vg_dot<64, VG_RS>(W + VG_R1W, xs, lane, W[VG_R1B + lane]));
+            float v[1] = {W[VG_R2W + lane] * r1};
+            row_reduce<false>(v);
+            v[0] += __shfl_xor(v[0], 16);
+            v[0] += __shfl_xor(v[0], 32);
+            if (lane == 0 && env0 < p.B) p.value[env0] = W[VG_R2B] + v[0];
+            ds_wave_fence();
+            continue;
+        }
         float mean[16];
         {
             const float invR = 1.0f / (float)R;
@@ -545,7 +665,7 @@ __device__ __forceinline__ void ds_fwd_body(const DSParams& p, float* W, int blk
 template <int TS, int P, int MODE>
 __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
     if (MODE == 2 && p.ex_on && ds_dqn_explore(p)) return;  // (uniform: the DQN step explores)
-    __shared__ __attribute__((aligned(16))) float W[DS_LDS_FLOATS];
+    __shared__ __attribute__((aligned(16))) float W[DSGeom<TS, P>::LDS];
     ds_fwd_body<TS, P, MODE>(p, W, blockIdx.x, gridDim.x);
 }
 
@@ -848,8 +968,45 @@ __device__ __forceinline__ float ds_frag_value(const float* w, int nout, int kin
     return (w && row < nout) ? w[row * kin + in] : 0.f;
 }
 
+// the VALU image (VG_*): fragments for the Lambda regions, row-major rows (stride S) elsewhere
+__device__ __forceinline__ float vg_rm_value(const float* w, int kin, int S, int idx) {
+    const int f = idx / S, j = idx - f * S;
+    return (w && j < kin) ? w[f * kin + j] : 0.f;
+}
+__device__ __forceinline__ void vg_pack_one(const lb_ds_weights& w, float* out, int j) {
+    const int starts[16] = {VG_A1L, VG_A2L, VG_A3L, VG_A3G, VG_A1G, VG_A2G, VG_C1L, VG_C2L,
+                            VG_C1G, VG_C2G, VG_C3L, VG_C3G, VG_R1W, VG_R1B, VG_R2W, VG_R2B};
+    int r = 15;
+    while (r > 0 && j < starts[r]) --r;
+    const int idx = j - starts[r];
+    float v = 0.f;
+    switch (r) {
+        case 0: v = ds_frag_value(w.actor_lambda[0], 64, 8, 2, idx); break;
+        case 1: v = ds_frag_value(w.actor_lambda[1], 64, 64, 16, idx); break;
+        case 2: v = ds_frag_value(w.actor_lambda[2], 1, 64, 16, idx); break;
+        case 3: v = -ds_frag_value(w.actor_gamma[2], 1, 64, 16, idx); break;
+        case 4: v = -vg_rm_value(w.actor_gamma[0], 8, VG_RS8, idx); break;
+        case 5: v = -vg_rm_value(w.actor_gamma[1], 64, VG_RS, idx); break;
+        case 6: v = ds_frag_value(w.critic_lambda[0], 64, 8, 2, idx); break;
+        case 7: v = ds_frag_value(w.critic_lambda[1], 64, 64, 16, idx); break;
+        case 8: v = -vg_rm_value(w.critic_gamma[0], 8, VG_RS8, idx); break;
+        case 9: v = -vg_rm_value(w.critic_gamma[1], 64, VG_RS, idx); break;
+        case 10: v = vg_rm_value(w.critic_lambda[2], 64, VG_RS, idx); break;
+        case 11: v = -vg_rm_value(w.critic_gamma[2], 64, VG_RS, idx); break;
+        case 12: v = vg_rm_value(w.rho_w1, 64, VG_RS, idx); break;
+        case 13: v = w.rho_b1 ? w.rho_b1[idx] : 0.f; break;
+        case 14: v = w.rho_w2 ? w.rho_w2[idx] : 0.f; break;
+        default: v = (w.rho_b2 && idx == 0) ? w.rho_b2[0] : 0.f; break;
+    }
+    out[DS_FLOATS + j] = v;
+}
+
 __device__ __forceinline__ void ds_pack_one(const lb_ds_weights& w, float* out, int i) {
-    if (i >= DS_FLOATS) return;
+    if (i >= DS_IMG_FLOATS) return;
+    if (i >= DS_FLOATS) {
+        vg_pack_one(w, out, i - DS_FLOATS);
+        return;
+    }
     // regions in layout order: (start, pointer, out features, in features, k-steps)
     const int starts[16] = {DS_A1L, DS_A1G, DS_A2L, DS_A2G, DS_A3L, DS_A3G, DS_C1L, DS_C1G,
                             DS_C2L, DS_C2G, DS_C3L, DS_C3G, DS_R1W, DS_R1B, DS_R2W, DS_R2B};

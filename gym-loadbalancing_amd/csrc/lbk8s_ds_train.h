@@ -771,7 +771,7 @@ __global__ void k_ds_pack_bwd(lb_ds_weights w, float* out) {
 }
 // lb_ds_pack_pair: both images of the same weights in one launch (the first blocks the forward
 // image, the rest the backward image); a DQN train period packs them once at its start
-constexpr int DS_PACK_BLOCKS = (DS_FLOATS + 255) / 256, DSB_PACK_BLOCKS = (DSB_FLOATS + 255) / 256;
+constexpr int DS_PACK_BLOCKS = (DS_IMG_FLOATS + 255) / 256, DSB_PACK_BLOCKS = (DSB_FLOATS + 255) / 256;
 __global__ void k_ds_pack_pair(lb_ds_weights w, float* out, float* bout) {
     if ((int)blockIdx.x < DS_PACK_BLOCKS) ds_pack_one(w, out, blockIdx.x * 256 + threadIdx.x);
     else ds_pack_bwd_one(w, bout, (blockIdx.x - DS_PACK_BLOCKS) * 256 + threadIdx.x);
@@ -843,6 +843,79 @@ __global__ __launch_bounds__(SG_THREADS) void k_ds_set_grads(SetGradParams p) {
             for (int s = 0; s < cs; ++s) acc += sa[s][m] * sb[s][n];
     }
     if (on) j.out[e] = j.scale * acc;
+}
+
+// ---- lb_ds_over_sets: out[m][n] = scale * sum_s A(s, m) B(s, n) over a large batch of sets
+// (the PPO minibatch's 51,200), every job in two launches.  The sums over the sets of the
+// training step -- the Gamma gradients (sum_r dz)^T max_set(h), the critic's Lambda3, rho's
+// two weight gradients and the bias sums -- were chunked torch GEMMs plus a reduction each
+// (~20 + 10 us per product: ~0.25 ms per minibatch).  Here one wave owns a 16 x 16 output tile
+// of one job over one span of OS_SPAN sets: v_mfma_f32_16x16x4_f32 with the sets as the K
+// dimension (A operand: lane l holds A(s0 + 4 t + l / 16, 16 mt + l % 16), B: B(s, 16 nt +
+// l % 16)), its partial sums to workspace[span][job output]; k_ds_over_sets_reduce adds the
+// spans in ascending order (deterministic) and scales.
+struct OverSetsJob {
+    const float* a;  // A(s, m) = a[s lda + m]; NULL: A(s, 0) = 1 (M == 1: a plain sum of B)
+    int64_t lda;
+    const float* b;  // B(s, n) = b[s ldb + n]
+    int64_t ldb;
+    int M, N;
+    float scale;
+    float* out;      // [M][N]
+    int ooff;        // offset of the job's outputs in a span's workspace row
+    int tile0;       // first global tile index of the job (tiles: ceil(M / 16) x ceil(N / 16))
+};
+constexpr int OS_JOBS = 16, OS_SPAN = 1024;
+struct OverSetsParams {
+    OverSetsJob job[OS_JOBS];
+    int njobs, ntiles, row;  // row: workspace floats per span (the sum of the jobs' M N)
+    int64_t S;
+    float* work;             // [spans][row]
+};
+
+__global__ __launch_bounds__(256) void k_ds_over_sets(OverSetsParams p) {
+    const int wt = blockIdx.x * 4 + (threadIdx.x >> 6);  // this wave's tile
+    if (wt >= p.ntiles) return;  // (wave-uniform)
+    int ji = 0;
+    while (ji + 1 < p.njobs && wt >= p.job[ji + 1].tile0) ++ji;
+    const OverSetsJob j = p.job[ji];
+    const int t = wt - j.tile0, ntn = (j.N + 15) / 16, mt = t / ntn, nt = t - mt * ntn;
+    const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+    const int m = 16 * mt + c, n = 16 * nt + c;
+    const int64_t s0 = (int64_t)blockIdx.y * OS_SPAN;
+    const int64_t s1 = s0 + OS_SPAN < p.S ? s0 + OS_SPAN : p.S;
+    dsf4 acc = {0.f, 0.f, 0.f, 0.f};
+    const bool am = m < j.M, bn = n < j.N;
+    const float* ap = j.a ? j.a + m : nullptr;
+    const float* bp = j.b + n;
+    // (a wave-uniform trip count: the MFMA takes every lane; sets past the span's end load 0)
+    const int steps = (int)((s1 - s0 + 3) / 4);
+#pragma unroll 4
+    for (int k = 0; k < steps; ++k) {
+        const int64_t s = s0 + 4 * k + q;
+        const bool in = s < s1;
+        const float av = (am && in) ? (ap ? ap[s * j.lda] : 1.f) : 0.f;
+        const float bv = (bn && in) ? bp[s * j.ldb] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+    }
+    float* w = p.work + (int64_t)blockIdx.y * p.row + j.ooff;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int mm = 16 * mt + 4 * q + i;
+        if (mm < j.M && bn) w[mm * j.N + n] = acc[i];
+    }
+}
+
+// out[e] = scale * sum over the spans (ascending) of the partial sums
+__global__ void k_ds_over_sets_reduce(OverSetsParams p, int spans) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= p.row) return;
+    int ji = 0;
+    while (ji + 1 < p.njobs && e >= p.job[ji + 1].ooff) ++ji;
+    const OverSetsJob& j = p.job[ji];
+    float acc = 0.f;
+    for (int z = 0; z < spans; ++z) acc += p.work[(int64_t)z * p.row + e];
+    j.out[e - j.ooff] = j.scale * acc;
 }
 
 }  // namespace lbk

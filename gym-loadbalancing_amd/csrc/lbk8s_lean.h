@@ -581,6 +581,9 @@ __device__ __forceinline__ void lean_copier(const Params& p, int K, int32_t* act
         cep = (uint32_t)(acc3 >> 32);
         const int to_done = p.L - (int)(sc & 0xFFFF);
         uint64_t mm = __ballot(to_done >= 1 && to_done <= K);
+#ifdef LB_DIAG_NOREC  // diagnostic (wrong values): no next-episode records drawn
+        mm = 0;
+#endif
         const uint32_t epi = (uint32_t)(acc3 >> 32) + 1;
         const int g = lane / RS_W, gl = lane % RS_W;
         while (mm) {  // (wave-uniform)
@@ -1077,6 +1080,9 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
     // from the accumulators their lanes saved at the restart: one pass for the wave, each lane
     // its row into its image region (the image is not read again), then 8 lanes (16 bytes each)
     // per 128-byte row, one store instruction per 8 envs
+#ifdef LB_DIAG_NOEPI  // diagnostic (wrong values): no episode-statistics rows, no scenario write-back
+    new_episode = false;
+#endif
     {
         const uint64_t endm = __ballot(new_episode);
         if (endm) {

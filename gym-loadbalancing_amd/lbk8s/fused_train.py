@@ -93,6 +93,33 @@ def _over_sets(a, b, alpha=1.0):
     return out
 
 
+OS_SPAN = 1024  # lb_ds_over_sets' sets per partial sum
+_os_work = {}
+
+
+def sums_over_sets(jobs, S, dev):
+    """lb_ds_over_sets: for each job (a, b, scale) with a (S, M) or None (a plain sum of b's rows)
+    and b (S, N) -- 2-D views with unit column stride -- the (M, N) tensor scale * a^T b, all jobs in
+    two launches (an MFMA partial sum per 1024-set span, then the spans added in order)."""
+    outs, cjobs, row = [], [], 0
+    for a, b, scale in jobs:
+        M = 1 if a is None else a.shape[1]
+        N = b.shape[1]
+        assert b.stride(1) == 1 and (a is None or a.stride(1) == 1)
+        o = torch.empty((M, N), dtype=torch.float32, device=dev)
+        outs.append(o)
+        cjobs.append(_native.LBSetJobC(None if a is None else a.data_ptr(), 0 if a is None else a.stride(0),
+                                       b.data_ptr(), b.stride(0), M, N, float(scale), o.data_ptr()))
+        row += M * N
+    need = ((S + OS_SPAN - 1) // OS_SPAN) * row
+    w = _os_work.get(dev)
+    if w is None or w.numel() < need:
+        w = _os_work[dev] = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=dev)
+    arr = (_native.LBSetJobC * len(cjobs))(*cjobs)
+    _native.check(_native.lib().lb_ds_over_sets(arr, len(cjobs), S, w.data_ptr(), w.numel(), _stream(dev)))
+    return outs
+
+
 class _FusedDeepSetsTrain(torch.autograd.Function):
     """(x, *params) -> (logits (B, R), psi_mean (B, 64) or None).
 
@@ -152,25 +179,22 @@ class _FusedDeepSetsTrain(torch.autograd.Function):
                 grads += [wgrad[1, 4096:].view(64, 8), c[:512].view(64, 8), wgrad[1, :4096].view(64, 64),
                           c[512:4608].view(64, 64), c[4608:8704].view(64, 64), c[8704:].view(64, 64)]
             return (None, None, None, None) + tuple(grads)
+        # the sums over the sets, every one in one lb_ds_over_sets call (two launches)
         max0 = _vec(setvec, "MAX0", 8)
-        g3 = dlogits.sum(1)
-        grads = [
-            wgrad[0, 4096:].view(64, 8),                                       # actor Lambda1
-            _over_sets(_vec(setvec, "GS1A"), max0, -1.0),                      # actor Gamma1
-            wgrad[0, :4096].view(64, 64),                                      # actor Lambda2
-            _over_sets(_vec(setvec, "GS2A"), _vec(setvec, "MAX1A"), -1.0),     # actor Gamma2
-            _vec(setvec, "GA3").sum(0, keepdim=True),                          # actor Lambda3
-            _over_sets(g3[:, None], _vec(setvec, "MAX2A"), -1.0),              # actor Gamma3
-        ]
+        g3 = dlogits.sum(1, keepdim=True)
+        jobs = [(_vec(setvec, "GS1A"), max0, -1.0),                            # actor Gamma1
+                (_vec(setvec, "GS2A"), _vec(setvec, "MAX1A"), -1.0),           # actor Gamma2
+                (None, _vec(setvec, "GA3"), 1.0),                              # actor Lambda3
+                (g3, _vec(setvec, "MAX2A"), -1.0)]                             # actor Gamma3
         if critic is not None:
-            grads += [
-                wgrad[1, 4096:].view(64, 8),                                   # critic Lambda1
-                _over_sets(_vec(setvec, "GS1C"), max0, -1.0),                  # critic Gamma1
-                wgrad[1, :4096].view(64, 64),                                  # critic Lambda2
-                _over_sets(_vec(setvec, "GS2C"), _vec(setvec, "MAX1C"), -1.0), # critic Gamma2
-                _over_sets(dmean / R, _vec(setvec, "CS2")),                    # critic Lambda3
-                _over_sets(dmean, _vec(setvec, "MAX2C"), -1.0),                # critic Gamma3
-            ]
+            jobs += [(_vec(setvec, "GS1C"), max0, -1.0),                       # critic Gamma1
+                     (_vec(setvec, "GS2C"), _vec(setvec, "MAX1C"), -1.0),      # critic Gamma2
+                     (dmean, _vec(setvec, "CS2"), 1.0 / R),                    # critic Lambda3
+                     (dmean, _vec(setvec, "MAX2C"), -1.0)]                     # critic Gamma3
+        s = sums_over_sets(jobs, B, dev)
+        grads = [wgrad[0, 4096:].view(64, 8), s[0], wgrad[0, :4096].view(64, 64), s[1], s[2], s[3]]
+        if critic is not None:
+            grads += [wgrad[1, 4096:].view(64, 8), s[4], wgrad[1, :4096].view(64, 64), s[5], s[6], s[7]]
         return (None, None, None, None) + tuple(grads)
 
 
@@ -233,7 +257,12 @@ class _Rho(torch.autograd.Function):
         mean, w1, w2, r1 = ctx.saved_tensors
         gv = gv.contiguous()
         gz = (gv @ w2) * torch.where(r1 > 0, torch.ones_like(r1), r1 + 1)
-        return gz @ w1, _over_sets(gz, mean), gz.sum(0), _over_sets(gv, r1), gv.sum(0)
+        S = mean.shape[0]
+        if S <= SET_GRADS_MAX_SETS or not gv.is_cuda:
+            return gz @ w1, _over_sets(gz, mean), gz.sum(0), _over_sets(gv, r1), gv.sum(0)
+        dw1, db1, dw2, db2 = sums_over_sets([(gz, mean, 1.0), (None, gz, 1.0), (gv, r1, 1.0), (None, gv, 1.0)], S,
+                                            gv.device)
+        return gz @ w1, dw1, db1.view(-1), dw2, db2.view(-1)
 
 
 def _eq_params(net):

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LBK8S_ABI_VERSION 11
+#define LBK8S_ABI_VERSION 12
 
 /* reward_function names of loadbalancer_k8s_env.py:20-31 */
 enum { LB_REWARD_NAIVE = 0, LB_REWARD_LATENCY = 1, LB_REWARD_FAIRNESS = 2, LB_REWARD_MULTI = 3 };
@@ -235,10 +235,11 @@ int lb_status(const void* state, const lb_config* cfg, int64_t num_envs, uint32_
  * (E <= 256 plus the reject row; above 80 the forward streams the set through the kernel in
  * 32-element chunks).
  * Weights are the torch parameters as they are (nn.Linear layout [out][in], f32, device);
- * lb_ds_pack rearranges them into the kernel's fragment order (LB_DS_FRAG_FLOATS floats),
- * to be redone after every optimizer step.  A NULL critic pointer set packs an actor-only
+ * lb_ds_pack rearranges them into the kernels' weight image (LB_DS_FRAG_FLOATS floats: the
+ * MFMA fragment order, then (ABI 12) the VALU image of the forwards with 33..80 set elements,
+ * row-major matrix-vector weights), to be redone after every optimizer step.  A NULL critic pointer set packs an actor-only
  * image (DQN); lb_ds_forward then must be called with value_out == NULL. */
-#define LB_DS_FRAG_FLOATS 33860
+#define LB_DS_FRAG_FLOATS 68552
 #define LB_DS_MAX_ELEMENTS 80       /* forward held in registers (above: streamed in chunks) */
 #define LB_DS_MAX_ELEMENTS_TRAIN 257 /* training forward / backward, PPO loss head */
 #define LB_DS_MAX_ELEMENTS_FWD 257  /* inference forward, greedy argmax */
@@ -469,6 +470,25 @@ int lb_ds_train_backward(const float* bwd_frag, const float* obs, int64_t num_en
 #define LB_DS_SETGRAD_CRITIC 12800
 int lb_ds_set_grads(const float* setvec, const float* dlogits, const float* dmean, int64_t num_sets,
                     int32_t num_elements, float* out, void* stream);
+
+/* (ABI 12) Sums over a large batch of sets, the training step's remaining weight gradients at
+ * PPO's minibatch size: for each job, out[m][n] = scale * sum_s A(s, m) B(s, n) with
+ * A(s, m) = a[s lda + m] (a NULL: A(s, 0) = 1, M = 1, a plain sum of B's rows) and
+ * B(s, n) = b[s ldb + n], 1 <= M, N <= 64, at most 16 jobs.  Two launches: each wave a 16 x 16
+ * output tile over a span of 1024 sets on f32 MFMA into workspace, then the spans' partial sums
+ * added in ascending order (deterministic).  workspace: ceil(num_sets / 1024) x sum(M N) floats.
+ * Replaces per job a chunked GEMM and its reduction. */
+typedef struct lb_set_job {
+    const float* a;
+    int64_t lda;
+    const float* b;
+    int64_t ldb;
+    int32_t M, N;
+    float scale;
+    float* out;
+} lb_set_job;
+int lb_ds_over_sets(const lb_set_job* jobs, int32_t num_jobs, int64_t num_sets, float* workspace,
+                    int64_t workspace_floats, void* stream);
 
 #ifdef __cplusplus
 }

@@ -39,6 +39,10 @@ def parse():
     ap.add_argument("--num-steps", type=int, default=100)
     ap.add_argument("--steps", type=int, default=2000, help="DQN timed vector steps")
     ap.add_argument("--warmup", type=int, default=300, help="DQN warm-up vector steps")
+    ap.add_argument("--lib", default=None, help="another build of liblbk8s.so (an A/B across builds)")
+    ap.add_argument("--torch-set-sums", action="store_true",
+                    help="A/B reference: the training step's sums over the sets as round-5's chunked torch GEMMs "
+                         "(fused_train._over_sets) instead of lb_ds_over_sets")
     return ap.parse_args()
 
 
@@ -47,7 +51,19 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from lbk8s import LBVecEnv
+    from lbk8s import LBVecEnv, _native, fused_train
+    if args.lib:
+        _native.LIB_PATH = os.path.abspath(args.lib)
+    if args.torch_set_sums:
+        def torch_sums(jobs, S, dev):
+            out = []
+            for a, b, scale in jobs:
+                if a is None:
+                    out.append((scale * b.sum(0, keepdim=True)) if scale != 1.0 else b.sum(0, keepdim=True))
+                else:
+                    out.append(fused_train._over_sets(a, b, scale))
+            return out
+        fused_train.sums_over_sets = torch_sums
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -126,6 +142,7 @@ def main():
                    period_graph=dqn.period_graph, device_rng=dqn.device_rng,
                    graphs_captured_before_timing=os.environ.get("LBK8S_BENCH_PREPARE", "1") == "1",
                    ep_return=dqn.episode_returns[-1] if dqn.episode_returns else None)
+    out.update(lib=os.path.basename(_native.LIB_PATH), set_sums="torch" if args.torch_set_sums else "lb_ds_over_sets")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
