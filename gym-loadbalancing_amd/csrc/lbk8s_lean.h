@@ -46,27 +46,15 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ Rsrc rsrc_of(const void* base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, -1, 0x00020000);
 }
-#ifndef LB_LEAN_ST_AUX
-#define LB_LEAN_ST_AUX 2
-#endif
-constexpr int BUF_NT = LB_LEAN_ST_AUX;  // the output stores' cache policy (gfx940+: sc0 = 1, nt = 2, sc1 = 16)
+// the output stores' cache policy: nontemporal (gfx940+: sc0 = 1, nt = 2, sc1 = 16; nt sc1, sc1 and
+// plain stores measured slower at 2^20 envs, profiles/r05_ab_store_policy.jsonl)
+constexpr int BUF_NT = 2;
 
-// Occupancy and hoisting guards of the step loop.  At 4 waves per SIMD (128 VGPRs) loop-invariant
-// values the compiler hoists out of the step loop spill, so they are laundered through empty asm
-// and recomputed per step; an experiment build can pick another occupancy and drop the guards.
-#ifndef LB_LEAN_MINW
-#define LB_LEAN_MINW 4
-#endif
-#ifndef LB_LEAN_XCD_MAP
-#define LB_LEAN_XCD_MAP 0
-#endif
-#ifdef LB_LEAN_NOGUARD
-#define LB_GUARD_S(...) ((void)0)
-#define LB_GUARD_V(...) ((void)0)
-#else
+// Hoisting guards of the step loop.  At 4 waves per SIMD (128 VGPRs) loop-invariant values the
+// compiler hoists out of the step loop spill, so they are laundered through empty asm and
+// recomputed per step.
 #define LB_GUARD_S(...) asm volatile("" : "+s"(__VA_ARGS__))
 #define LB_GUARD_V(...) asm volatile("" : "+v"(__VA_ARGS__))
-#endif  // cache-policy bit of a nontemporal access (gfx940+: sc0 = 1, nt = 2)
 
 __device__ __forceinline__ double buf_ld_f64(Rsrc r, uint32_t off) {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
@@ -501,26 +489,19 @@ __device__ __forceinline__ float4 lean_piece(const uint32_t* wimg, int lane, int
     return img_piece(A, S, h);
 }
 
-#ifdef LB_TIMELINE  // diagnostic build (tools/timeline_lean.py): per-wave stamps at 6 points of each step
-constexpr int LTL_NP = 6, LTL_H = 8;  // per wave: 8 header words, then 6 stamps per step
-#define LB_LTL(k, i)                                                                                            \
-    do {                                                                                                        \
-        asm volatile("" ::: "memory");                                                                          \
-        if (g_timeline && lane == 0)                                                                            \
-            g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP) + LTL_H + (k) * LTL_NP + (i)] = __builtin_amdgcn_s_memtime(); \
-        asm volatile("" ::: "memory");                                                                          \
-    } while (0)
+// per-wave timeline stamps: diagnostic builds only (-DLB_TIMELINE: tools/diag, tools/timeline_lean.py)
+#ifdef LB_TIMELINE
+#include "../../tools/diag/lbk8s_lean_timeline.h"
 #else
 #define LB_LTL(k, i) ((void)0)
+#define LB_LTL_HDR(slot) ((void)0)
+#define LB_LTL_HWID() ((void)0)
 #endif
 
 // One wave per block: a block's LDS and wave slot are released the moment its wave ends, so
 // the next wave starts there at once (with 4-wave blocks a finished wave's slot waited for its
 // three siblings: 74 % of the wave slots were in use over a 20-step launch)
-#ifndef LB_LEAN_NB
-#define LB_LEAN_NB 64
-#endif
-constexpr int LEAN_NB = LB_LEAN_NB;
+constexpr int LEAN_NB = 64;
 
 // The split layout (CW = 1: k_rollout_lean_split, lb_rollout's launches of at most
 // LEAN_SPLIT_MAX_K steps): each block pairs the env wave with a copy wave.  The env wave never
@@ -531,9 +512,12 @@ constexpr int LEAN_NB = LB_LEAN_NB;
 // env wave computes.  (The env work alone runs 26-30 us per step at 2^20 envs, the store stream
 // alone 46-55, the two in one wave 63-66; split, the env waves are half as many per SIMD, and
 // the 20-step launch gains 3-4%, the 100-step one loses 1-2%: profiles/r05_ab_split.jsonl.)
-#ifndef LB_SPLIT_DRAWS
-#define LB_SPLIT_DRAWS 0
-#endif
+// Round 6: the copy wave also draws every step's Philox blocks one step ahead -- the random
+// policy's action and the next request's X / I blocks with their two float64 logs, a third of
+// the env wave's per-step chain -- and hands them over in LDS (split_draws); the env wave's
+// preparation reads them.  The copy wave replays the env's step count and episode itself (an
+// env ends at most once in a launch, L >= K, at step count L).  Bit for bit the same draws
+// (tests/test_gpu_lean_oracle.py); 131,072 envs 9.21 -> 8.86 us per step (profiles/r06_ab_*).
 // the split layout's draw buffers (after the reward / done / action words in sstage): per step
 // parity b, 64 x1 and 64 x2 (f64) and 64 words a | r << 8 | n << 16 (byte offsets from sstage)
 constexpr uint32_t SD_BASE = 3 * 64 * 4, SD_BUF = 64 * 20, SD_X2 = 64 * 8, SD_W = 64 * 16;
@@ -563,13 +547,7 @@ __device__ __forceinline__ void lean_copier(const Params& p, int K, int32_t* act
                                             uint32_t* sst, int64_t env0) {
     const int lane = threadIdx.x & 63;
     const bool h = (lane & 1) != 0;
-    uint32_t cs = 0, cep = 0;  // (LB_SPLIT_DRAWS) the env's step count and episode before the next step
-#ifndef LB_SPLIT_CPRIO
-#define LB_SPLIT_CPRIO -1
-#endif
-#if LB_SPLIT_CPRIO >= 0
-    __builtin_amdgcn_s_setprio(LB_SPLIT_CPRIO);
-#endif
+    uint32_t cs = 0, cep = 0;  // the env's step count and episode before the next step (split_draws)
     // the next episodes of the block's envs that end inside the launch, into their records (the
     // env wave's prologue in the single-wave layout; here beside the env wave's state loads and
     // image): 8 lanes per record, 8 records per pass, then barrier P
@@ -581,9 +559,6 @@ __device__ __forceinline__ void lean_copier(const Params& p, int K, int32_t* act
         cep = (uint32_t)(acc3 >> 32);
         const int to_done = p.L - (int)(sc & 0xFFFF);
         uint64_t mm = __ballot(to_done >= 1 && to_done <= K);
-#ifdef LB_DIAG_NOREC  // diagnostic (wrong values): no next-episode records drawn
-        mm = 0;
-#endif
         const uint32_t epi = (uint32_t)(acc3 >> 32) + 1;
         const int g = lane / RS_W, gl = lane % RS_W;
         while (mm) {  // (wave-uniform)
@@ -594,13 +569,10 @@ __device__ __forceinline__ void lean_copier(const Params& p, int K, int32_t* act
             for (int j = 0; j < 8; ++j) mm &= mm - 1;
         }
     }
-#if LB_SPLIT_DRAWS
     split_draws<KIND>(p, env0 + lane, cep, cs, sst, 0, lane);  // step 0's
-#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the records are written before P)
     block_lds_sync();  // P
     for (int k = 0; k < K; ++k) {
-#if LB_SPLIT_DRAWS
         // the env after step k (an env ends at most once in the launch, L >= K: restart at L),
         // then step k + 1's draws into buffer (k + 1) & 1 (its last reader, the env wave's
         // preparation of step k - 1, finished before barrier B of step k - 2 / the prologue)
@@ -609,7 +581,6 @@ __device__ __forceinline__ void lean_copier(const Params& p, int K, int32_t* act
             ++cep;
         }
         if (k + 1 < K) split_draws<KIND>(p, env0 + lane, cep, cs, sst, (k + 1) & 1, lane);
-#endif
         block_lds_sync();  // A: step k's images and words are in LDS
         float4 v[CW][P];
         uint32_t rw[CW], dn[CW], ac[CW];
@@ -645,22 +616,15 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
                                           uint32_t* sstage) {
     static_assert(CW == 0 || CW == 1, "one env wave per copy wave (two: the copy wave's registers for both blocks spilled)");
     constexpr bool SPLIT = CW > 0;
-#ifndef LB_SPLIT_ENVPRIO
-#define LB_SPLIT_ENVPRIO 1
-#endif
     constexpr int NB = SPLIT ? 64 * (CW + 1) : LEAN_NB, NW = SPLIT ? CW : NB / 64, P = 2 * RT, GT = 64 / P;
     constexpr int FAST = GT < REC_FETCH_MAX ? GT : REC_FETCH_MAX;  // restarts per step of the fast path
     static_assert(ET >= 1 && ET <= TPE_E && (RT == ET || RT == ET + 1), "compile-time geometry");
     (void)NW;
     const LDims<ET, RT> d(p);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    // block -> env group: blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
-    // workgroup dispatch); LB_LEAN_XCD_MAP gives each XCD a contiguous eighth of the groups
-#if LB_LEAN_XCD_MAP
-    const int64_t blk = gridDim.x % 8 == 0 ? (int64_t)(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8 : blockIdx.x;
-#else
+    // block -> env group (blocks are dealt round-robin over the 8 XCDs; giving each XCD a
+    // contiguous eighth of the groups measured within noise: profiles/r05_ab_xcd.jsonl)
     const int64_t blk = blockIdx.x;
-#endif
     if constexpr (SPLIT) {
         if (wv == CW) {  // the copy wave (its block's env waves 0 .. CW - 1: envs blockIdx.x * 64 CW ..)
             lean_copier<P, ACT, CW, KIND>(p, K, act_out, simg, sstage, blk * 64 * CW);
@@ -674,14 +638,8 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
     // synchronisation below is within the wave; the split layout's blocks are whole)
     const int64_t env0 = blk * (SPLIT ? 64 * CW : NB) + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63);
     if (env0 >= p.B) return;
-#ifdef LB_TIMELINE
-    if (g_timeline && threadIdx.x % 64 == 0)
-        g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP) + 2] = __builtin_amdgcn_s_memrealtime();
-    if (g_timeline && threadIdx.x % 64 == 0) {  // where the wave runs: HW_ID (cu, simd, se, ...), XCC_ID
-        g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP) + 6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-        g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP) + 7] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
-    }
-#endif
+    LB_LTL_HDR(2);
+    LB_LTL_HWID();
     const int64_t env = env0 + lane;
     const uint32_t envi = (uint32_t)env;
     const Rsrc blob = rsrc_of(p.lat_lut);  // tables, lat0 array and records (blob < 4 GiB: host check)
@@ -746,9 +704,7 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
         }
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
-#ifdef LB_TIMELINE
-    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP) + 4] = __builtin_amdgcn_s_memrealtime();
-#endif
+    LB_LTL_HDR(4);
 
     // the observation image from the state (table reads of the current latency and cpu)
     {
@@ -771,9 +727,7 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
     // loop and uses on some paths only were otherwise still pending at the loop header,
     // where its wait for them drained the stores of the previous step)
     __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0)
-#ifdef LB_TIMELINE
-    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP) + 5] = __builtin_amdgcn_s_memrealtime();
-#endif
+    LB_LTL_HDR(5);
     bool new_episode = false;
     uint32_t l0off = (uint32_t)(reinterpret_cast<const char*>(p.lat0) - reinterpret_cast<const char*>(p.lat_lut)) +
                      envi * 8u;
@@ -808,13 +762,9 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
         tv.s.rz = (int)((v.s1 >> S1_RZ) & 3);
         const int step = (int)(v.s0 & 0xFFFF);
         tv.s.step = step;
-#if LB_SPLIT_DRAWS
         // (split layout: the copy wave drew this step's action and request one step ahead)
         const uint32_t dw = SPLIT ? sd_w(sstage, j & 1)[lane] : 0u;
         const int a = SPLIT && KIND == LB_POLICY_RANDOM ? (int)(dw & 0xFFu) : lean_policy<KIND>(p, env, tv, em, ed);
-#else
-        const int a = lean_policy<KIND>(p, env, tv, em, ed);
-#endif
         const bool accept = a < ET;
         const int ai = accept ? a : 0;
         const uint32_t emA = pick8(em, ai), edA = pick8(ed, ai);
@@ -825,21 +775,11 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
         const int jn = jA < CMAX ? jA + 1 : CMAX;
         const int k0A = lem_k0(emA), c0A = em_c0(emA);
         // selected_endpoint_latency: lat0 on a first selection (LAT row 0 holds trunc(lat0))
-#ifdef LB_DIAG_NO_GATHER  // diagnostic build only (tools/r5): the step without its 4 table loads (wrong values)
-        r.sel_lat = 10.0 + jA + k0A;
-        r.sel_cpu = 20.0 + ed_m(edA) + c0A;
-        r.next_lat = 11.0 + jn + k0A;
-        r.next_cpu = 21.0 + Mn + c0A;
-        (void)l0off; (void)l0step; (void)cpu0;
-#else
         r.sel_lat = buf_ld_f64(blob, jA == 0 ? l0off + (uint32_t)ai * l0step : (uint32_t)(jA * LAT_ROWS + k0A) * 8u);
         r.sel_cpu = buf_ld_f64(blob, cpu0 + (uint32_t)(ed_m(edA) * CPU_ROWS + c0A) * 8u);
         r.next_lat = buf_ld_f64(blob, (uint32_t)(jn * LAT_ROWS + k0A) * 8u);
         r.next_cpu = buf_ld_f64(blob, cpu0 + (uint32_t)(Mn * CPU_ROWS + c0A) * 8u);
-#endif
-#ifndef LB_LEAN_NO_PREF
         fetch_next(step);
-#endif
         // (each stage's stores are pinned between computed values: "memory" barriers that
         // name the values just computed, so neither the compiler's IR passes nor its
         // scheduler can bunch the stores or sink the computation past them)
@@ -848,15 +788,12 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
         asm volatile("" ::: "memory");
         double x1, x2;
         int rr, n;
-#if LB_SPLIT_DRAWS
         if constexpr (SPLIT) {
             x1 = sd_x1(sstage, j & 1)[lane];
             x2 = sd_x2(sstage, j & 1)[lane];
             rr = (int)((dw >> 8) & 0xFFu);
             n = (int)(dw >> 16);
-        } else
-#endif
-        {
+        } else {
         const uint32_t episode = (uint32_t)(v.acc3 >> 32), slot = (uint32_t)(step + 1);
         U4 wx, wi;
         draw2_o(p, env, episode, slot, D_REQ_X, D_REQ_I, wx, wi);
@@ -899,10 +836,6 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
     auto iter = [&](const int k) {
         LB_LTL(k, 0);
         // issue priority by progress (k_rollout_img): a wave behind the others goes first
-#if LB_SPLIT_ENVPRIO == 0
-        if (!SPLIT)
-#endif
-#ifndef LB_LEAN_NOPRIO
         {
             const int pl = 3 - (4 * k) / K;
             if (pl >= 3) __builtin_amdgcn_s_setprio(3);
@@ -910,25 +843,13 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
             else if (pl == 1) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(0);
         }
-#endif
         const int a_k = (int)(pr.arz & 0xFFu);
         v.s0 += 1;  // step (<= L: the episode ends there)
         const bool done = (int)(v.s0 & 0xFFFF) == p.L;  // (:472)
         const double reward = lean_apply_l<ET, RT, NAIVE ? (int)LB_REWARD_NAIVE : -1>(p, pr, v, em, ed, me);
         const uint64_t m = __ballot(done);
         LB_LTL(k, 1);
-#ifdef LB_DIAG_MIN_RESET  // diagnostic (wrong values): the restart's register part only, no image / record work
-        if (done) {
-            v.acc3 = (uint64_t)((uint32_t)(v.acc3 >> 32) + 1) << 32;
-            v.acc2 = 0; v.sum_lat = 0; v.sum_cpu = 0; v.sum_hi = 0; v.total = 0.0; v.s0 = 0;
-#pragma unroll
-            for (int i = 0; i < TPE_E; ++i) ed[i] = 0u;
-            new_episode = true;
-        }
-        if (false) {
-#else
         if (m) {  // VecEnv auto-reset: episode stats + terminal obs, then the record's episode
-#endif
             // (the stores below are younger than the prefetched record, so waiting for it does
             // not wait for them; the next gathers do, but a few 16-byte stores issued just
             // before them cost about nothing next to the gathers' own round trip)
@@ -938,11 +859,7 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
             // else loaded here: a block of its own, so the wait for the prefetched record stays
             // a counted vmcnt instead of a vmcnt(0) behind the stores above), the restarts in place
             const int pc = lane % P;
-#ifdef LB_LEAN_NO_PREF  // (diagnostic build: no record prefetch, every restart loads its records here)
-            bool pre = false;
-#else
             bool pre = __popcll(m) <= FAST;
-#endif
             for (uint64_t mm = m; mm;) {  // (wave-uniform)
                 uint64_t grp = mm;
 #pragma unroll
@@ -988,10 +905,6 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
             sstage[192 * wv + lane] = __float_as_uint((float)reward);
             sstage[192 * wv + 64 + lane] = done ? 1u : 0u;
             if (ACT) sstage[192 * wv + 128 + lane] = (uint32_t)a_k;
-#ifndef LB_SPLIT_ORDER
-#define LB_SPLIT_ORDER 0
-#endif
-#if LB_SPLIT_ORDER == 0
             block_lds_sync();  // A
             LB_LTL(k, 3);
             if (k + 1 < K) {
@@ -1002,22 +915,6 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
             LB_LTL(k, 4);
             block_lds_sync();  // B (the image and words are read)
             LB_LTL(k, 5);
-#elif LB_SPLIT_ORDER == 1
-            if (k + 1 < K) {
-                pr = prep(k + 1, [](int) {});
-                asm volatile("" : "+v"(pr.sel_lat), "+v"(pr.sel_cpu), "+v"(pr.next_lat), "+v"(pr.next_cpu),
-                             "+v"(qn.x), "+v"(qn.y), "+v"(qn.z), "+v"(qn.w));
-            }
-            block_lds_sync();  // A
-            block_lds_sync();  // B (the image and words are read)
-#else
-            if (k + 1 < K) pr = prep(k + 1, [](int) {});
-            block_lds_sync();  // A
-            block_lds_sync();  // B (the image and words are read)
-            if (k + 1 < K)
-                asm volatile("" : "+v"(pr.sel_lat), "+v"(pr.sel_cpu), "+v"(pr.next_lat), "+v"(pr.next_cpu),
-                             "+v"(qn.x), "+v"(qn.y), "+v"(qn.z), "+v"(qn.w));
-#endif
             return;
         }
         // step k's outputs leave after step k + 1's gathers, spread over its request draws
@@ -1066,23 +963,16 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
     // (the first step is peeled off the loop: the loop is then entered, like its back edge,
     // with the gathers followed by a step's stores in flight, and the compiler's wait for
     // the gathers is a counted vmcnt instead of the vmcnt(0) the loop entry's shape forced)
-#ifdef LB_TIMELINE
-    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP)] = __builtin_amdgcn_s_memrealtime();
-#endif
+    LB_LTL_HDR(0);
     if (K > 0) iter(0);
     for (int k = 1; k < K; ++k) iter(k);
     // (the write-back's addresses from an opaque copy of the env index: the compiler would
     // otherwise keep the launch start's 64-bit addresses alive across the loop)
-#ifdef LB_TIMELINE
-    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP) + 1] = __builtin_amdgcn_s_memrealtime();
-#endif
+    LB_LTL_HDR(1);
     // the episode-statistics rows of the envs that ended in the launch (write_stats_row's values),
     // from the accumulators their lanes saved at the restart: one pass for the wave, each lane
     // its row into its image region (the image is not read again), then 8 lanes (16 bytes each)
     // per 128-byte row, one store instruction per 8 envs
-#ifdef LB_DIAG_NOEPI  // diagnostic (wrong values): no episode-statistics rows, no scenario write-back
-    new_episode = false;
-#endif
     {
         const uint64_t endm = __ballot(new_episode);
         if (endm) {
@@ -1133,26 +1023,22 @@ __device__ __forceinline__ void lean_body(Params p, int K, int32_t* act_out, uin
     p.sum_hi[ew] = v.sum_hi;
     p.total[ew] = v.total;
     if (!NAIVE) p.last_r[ew] = v.last_r;
-#ifdef LB_TIMELINE
-    if (g_timeline && lane == 0) g_timeline[(env0 / 64) * (LTL_H + K * LTL_NP) + 3] = __builtin_amdgcn_s_memrealtime();
-#endif
+    LB_LTL_HDR(3);
 }
 
 template <int KIND, int ET, int RT, int NZW, bool NAIVE, bool ACT>
-__global__ __launch_bounds__(LEAN_NB, LB_LEAN_MINW) void k_rollout_lean(Params p, int K, int32_t* act_out) {
+__global__ __launch_bounds__(LEAN_NB, 4) void k_rollout_lean(Params p, int K, int32_t* act_out) {
     __shared__ __attribute__((aligned(16))) uint32_t simg[LEAN_NB / 64][64 * IMG_W];
     lean_body<KIND, ET, RT, NZW, NAIVE, ACT, 0>(p, K, act_out, simg, nullptr);
 }
 // the split layout: 128-thread blocks (env wave + copy wave)
-#ifndef LB_LEAN_SPLIT_LB
-#define LB_LEAN_SPLIT_LB 4  // (min waves per SIMD: 128 VGPRs)
-#endif
+// (4 waves per SIMD: 128 VGPRs; 2 and 3 measured equal, profiles/r05_ab_occupancy.jsonl)
 template <int KIND, int ET, int RT, int NZW, bool NAIVE, bool ACT, int CW>
-__global__ __launch_bounds__(64 * (CW + 1), LB_LEAN_SPLIT_LB) void k_rollout_lean_split(Params p, int K,
+__global__ __launch_bounds__(64 * (CW + 1), 4) void k_rollout_lean_split(Params p, int K,
                                                                                        int32_t* act_out) {
     __shared__ __attribute__((aligned(16))) uint32_t simg[CW][64 * IMG_W];
-    // each env wave's step reward, done, action words; then (LB_SPLIT_DRAWS) the draw buffers
-    __shared__ __attribute__((aligned(16))) uint32_t sstage[CW * 3 * 64 + (LB_SPLIT_DRAWS ? 2 * SD_BUF / 4 : 0)];
+    // each env wave's step reward, done, action words; then the draw buffers
+    __shared__ __attribute__((aligned(16))) uint32_t sstage[CW * 3 * 64 + 2 * SD_BUF / 4];
     lean_body<KIND, ET, RT, NZW, NAIVE, ACT, CW>(p, K, act_out, simg, sstage);
 }
 

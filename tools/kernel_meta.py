@@ -13,15 +13,25 @@ import tempfile
 LLVM = "/opt/rocm/llvm/bin"
 
 
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
 def kernels(lib):
+    notes = ""
     with tempfile.TemporaryDirectory() as d:
-        fb, co = os.path.join(d, "fb.bin"), os.path.join(d, "co.o")
+        fb = os.path.join(d, "fb.bin")
         subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", lib, os.path.join(d, "x")],
                        check=True)
-        subprocess.run([f"{LLVM}/clang-offload-bundler", "--type=o", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
-                        f"--input={fb}", f"--output={co}", "--unbundle"], check=True)
-        notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], capture_output=True, text=True,
-                               check=True).stdout
+        data = open(fb, "rb").read()
+        starts = [i for i in range(len(data)) if data.startswith(MAGIC, i)]
+        for n, a in enumerate(starts):  # (one bundle per compiled unit)
+            b = starts[n + 1] if n + 1 < len(starts) else len(data)
+            part, co = os.path.join(d, f"b{n}.bin"), os.path.join(d, f"co{n}.o")
+            open(part, "wb").write(data[a:b])
+            subprocess.run([f"{LLVM}/clang-offload-bundler", "--type=o", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
+                            f"--input={part}", f"--output={co}", "--unbundle"], check=True)
+            notes += subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], capture_output=True, text=True,
+                                    check=True).stdout
     out, cur = [], None
     for line in notes.splitlines():
         m = re.match(r"\s*-?\s*\.(\w+):\s+(\S+)", line)
