@@ -899,7 +899,9 @@ void ds_forward_launch(const DSParams& p, hipStream_t s) {
     // when the batch would leave SIMDs of the chip idle (the DQN vector step's 4096 envs:
     // 1,024 groups of four, one per SIMD; its 128-set train step)
     const int ts = (p.R + 15) / 16;
-    int P = ts == 1 ? 4 : (ts == 2 ? 2 : 1);
+    // (the greedy-action forward of small sets takes at most two envs per iteration: its Gamma
+    // terms on the VALU, the arithmetic of k_dqn_step's Q forward)
+    int P = ts == 1 ? (MODE == 2 ? 2 : 4) : (ts == 2 ? 2 : 1);
     {
         const int64_t simds = (int64_t)device_cus() * 4 * LB_DS_WAVES_PER_SIMD;
         while (P > 1 && (p.B + P - 1) / P < simds) P /= 2;
@@ -1038,10 +1040,7 @@ int dqn_steps_launch(const float* frag, float* obs, int64_t num_envs, int32_t nu
     DQNReplay r{slots, num_elements * 2, pos_in, pos_out, reinterpret_cast<float4*>(obs),
                 reinterpret_cast<float4*>(rb_obs), reinterpret_cast<float4*>(rb_next_obs), rb_actions, rb_rewards,
                 rb_dones, ep_sum, ep_cnt};
-#ifndef LB_DQN_P
-#define LB_DQN_P 2  // envs per wave iteration: 2 puts the 4096-env batch on every wave of the grid (4: half the waves idle)
-#endif
-    constexpr int P = LB_DQN_P;
+    constexpr int P = 2;  // envs per wave iteration: 2 puts the 4096-env batch on every wave of the grid (4: half the waves idle)
     const unsigned grid = ds_grid_spread((num_envs + P - 1) / P);
     hipLaunchKernelGGL(k_dqn_step<P>, dim3(grid), dim3(DS_BLOCK), 0, (hipStream_t)stream, d, e, r, (int)steps, sync);
     return check_launch();

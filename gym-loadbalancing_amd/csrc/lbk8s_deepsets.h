@@ -101,19 +101,24 @@ enum : int {
     VG_C1L = 11776, VG_C2L = 12288, VG_C1G = 16384, VG_C2G = 17152, VG_C3L = 21504, VG_C3G = 25856,
     VG_R1W = 30208, VG_R1B = 34560, VG_R2W = 34624, VG_R2B = 34688, VG_FLOATS = 34692,
     DS_IMG_FLOATS = DS_FLOATS + VG_FLOATS,
-    VG_SCRATCH = 128,  // per wave: the matvec input x[64] and output y[64]
+    VG_SCRATCH = 128,  // per wave and env of a wave iteration: the matvec input x[64] and output y[64]
 };
-template <int TS, int P>
+// VG: the forwards with one env per wave iteration and >= 3 set tiles, and the greedy-action
+// forward (MODE 2: the DQN's Q values) of small sets with one or two envs per iteration -- the
+// same arithmetic as k_dqn_step's Q forward, so lb_dqn_act and lb_dqn_step pick the same actions
+template <int TS, int P, int MODE = 0>
 struct DSGeom {
-    static constexpr bool VG = TS >= 3 && P == 1;
-    static constexpr int LDS = VG ? VG_FLOATS + (DS_BLOCK / 64) * VG_SCRATCH : DS_LDS_FLOATS;
+    static constexpr bool VG = (TS >= 3 && P == 1) || (MODE == 2 && TS == 1 && P <= 2);
+    static constexpr int LDS = VG ? VG_FLOATS + (DS_BLOCK / 64) * P * VG_SCRATCH : DS_LDS_FLOATS;
 };
 // (wave-local LDS ordering: the wave's own writes before its later reads by other lanes)
 __device__ __forceinline__ void ds_wave_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-// the set's max (P = 1: every lane holds it, feature in(k, grp)) into x[KS * 4]
+// the set's max (lane (col, grp) holds env col mod P's, feature in(k, grp)) into x[KS * 4]
+// (P envs: env s's at x + 128 s, written by the lanes of column s)
 template <int KS>
-__device__ __forceinline__ void vg_put(const float (&mb)[KS], float* x, int col, int grp) {
-    if (col != 0) return;
+__device__ __forceinline__ void vg_put(const float (&mb)[KS], float* x, int col, int grp, int P = 1) {
+    if (col >= P) return;
+    x += 128 * col;
     if constexpr (KS == 2) {
         x[grp] = mb[0];
         x[4 + grp] = mb[1];
@@ -124,6 +129,8 @@ __device__ __forceinline__ void vg_put(const float (&mb)[KS], float* x, int col,
     }
 }
 // acc + sum_j W[f][j] x[j] for this lane's output feature f = lane (ascending j)
+// (in groups of 16 inputs: the compiler would otherwise issue every LDS read of the row first and
+// hold it in registers, 64 VGPRs for a 64-input row)
 template <int KIN, int S>
 __device__ __forceinline__ float vg_dot(const float* Wrm, const float* x, int lane, float acc) {
     const float* w = Wrm + lane * S;
@@ -134,21 +141,25 @@ __device__ __forceinline__ float vg_dot(const float* Wrm, const float* x, int la
         acc = fmaf(a.y, b.y, acc);
         acc = fmaf(a.z, b.z, acc);
         acc = fmaf(a.w, b.w, acc);
+        if ((j & 15) == 12) asm volatile("" : "+v"(acc));
     }
     return acc;
 }
-// (-Gamma) max_set(h) by VALU into the accumulator layout: g[nt][i] = y[16 nt + 4 grp + i]
-template <int KS>
-__device__ __forceinline__ void vg_gamma(const float* Grm, const float (&mb)[KS], float* xs, int lane, dsf4 (&g)[4]) {
+// (-Gamma) max_set(h) of each of the P envs by VALU into the scratch: y_s = xs + 128 s + 64.
+// Lane f computes output f of every env (P dot products); the caller reads the accumulator
+// layout, y_s[16 nt + 4 grp + i], where it initialises the accumulators (vg_init)
+template <int KS, int P>
+__device__ __forceinline__ void vg_gamma(const float* Grm, const float (&mb)[KS], float* xs, int lane) {
     const int col = lane & 15, grp = lane >> 4;
-    vg_put<KS>(mb, xs, col, grp);
-    ds_wave_fence();
-    const float y = vg_dot<4 * KS, KS == 2 ? VG_RS8 : VG_RS>(Grm, xs, lane, 0.f);
-    xs[64 + lane] = y;
+    vg_put<KS>(mb, xs, col, grp, P);
     ds_wave_fence();
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) g[nt] = *reinterpret_cast<const dsf4*>(xs + 64 + 16 * nt + 4 * grp);
-    ds_wave_fence();  // (read before the scratch is rewritten)
+    for (int s = 0; s < P; ++s)
+        xs[128 * s + 64 + lane] = vg_dot<4 * KS, KS == 2 ? VG_RS8 : VG_RS>(Grm, xs + 128 * s, lane, 0.f);
+    ds_wave_fence();
+}
+__device__ __forceinline__ dsf4 vg_init(const float* xs, int s, int nt, int grp) {
+    return *reinterpret_cast<const dsf4*>(xs + 128 * s + 64 + 16 * nt + 4 * grp);
 }
 
 __device__ __forceinline__ dsf4 mfma4(float a, float b, dsf4 c) {
@@ -327,10 +338,10 @@ __device__ __forceinline__ void eq_layer(const float* L, const float* G, const f
                                          const float (&mb)[KS], float (&out)[P * TS][16], int lane,
                                          float* xs = nullptr) {
     constexpr int ST = P * TS;
-    dsf4 g[4];
+    dsf4 g[4];  // (MFMA: env s's result in column s; VG: in the scratch, every lane reads its part)
     if constexpr (VG) {
-        static_assert(P == 1, "one env per wave iteration");
-        vg_gamma<KS>(G, mb, xs, lane, g);
+        static_assert(P <= 2, "VALU Gamma: one or two envs per wave iteration");
+        vg_gamma<KS, P>(G, mb, xs, lane);
     } else {
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) g[nt] = dsf4{0.f, 0.f, 0.f, 0.f};
@@ -348,11 +359,16 @@ __device__ __forceinline__ void eq_layer(const float* L, const float* G, const f
 #pragma unroll
             for (int s = 0; s < P; ++s) {
                 dsf4 init;
+                if constexpr (VG) {
+                    init = vg_init(xs, s, nt0 + j, lane >> 4);
+                } else {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) init[i] = from_col_dyn<P>(g[nt0 + j][i], s);
+                    for (int i = 0; i < 4; ++i) init[i] = from_col_dyn<P>(g[nt0 + j][i], s);
+                }
 #pragma unroll
                 for (int t = 0; t < TS; ++t) acc[j][s * TS + t] = init;
             }
+        if constexpr (VG) ds_wave_fence();  // (the scratch is read before a later layer rewrites it)
 #pragma unroll
         for (int k = 0; k < KS; ++k)
 #pragma unroll
@@ -428,11 +444,11 @@ __device__ __forceinline__ void ds_group_obs(const DSParams& p, int64_t env0, in
 // one wave iteration's P envs: the actor (or Q network) Eq(8->64) ReLU Eq(64->64) ELU Eq(64->1);
 // logits / training rows / the masked greedy action (ARGMAX: lane s < P returns env0 + s's)
 // (W: the fragment image, or the VALU image with xs the wave's scratch: DSGeom<TS, P>::VG)
-template <int TS, int P, int MODE>
+template <int TS, int P, int MODE, bool VG = DSGeom<TS, P, MODE>::VG>
 __device__ __forceinline__ int32_t ds_group_actor(const DSParams& p, const float* W, int lane, int64_t env0, int col,
                                                   int grp, int R, const float (&h0)[P * TS][2], const float (&m0)[2],
                                                   float* xs = nullptr) {
-    constexpr bool TRAIN = MODE == 1, ARGMAX = MODE == 2, VG = DSGeom<TS, P>::VG;
+    constexpr bool TRAIN = MODE == 1, ARGMAX = MODE == 2;
     constexpr int A1L = VG ? VG_A1L : DS_A1L, A1G = VG ? VG_A1G : DS_A1G, A2L = VG ? VG_A2L : DS_A2L,
                   A2G = VG ? VG_A2G : DS_A2G, A3L = VG ? VG_A3L : DS_A3L, A3G = VG ? VG_A3G : DS_A3G;
     int32_t act = -1;
@@ -509,7 +525,7 @@ __device__ __forceinline__ int32_t ds_group_actor(const DSParams& p, const float
 // its half of the grid), W the block's LDS weight region
 template <int TS, int P, int MODE>
 __device__ __forceinline__ void ds_fwd_body(const DSParams& p, float* W, int blk, int nblk) {
-    constexpr bool TRAIN = MODE == 1, ARGMAX = MODE == 2, VG = DSGeom<TS, P>::VG;
+    constexpr bool TRAIN = MODE == 1, ARGMAX = MODE == 2, VG = DSGeom<TS, P, MODE>::VG;
     // stage the weight image (once per block; blocks are persistent): the fragment image, or
     // the VALU image (VG); an actor-only launch (DQN) stages only the actor's part
     const int nstage = VG ? ((ARGMAX || !p.critic) ? (int)VG_ACTOR : (int)VG_FLOATS)
@@ -518,7 +534,7 @@ __device__ __forceinline__ void ds_fwd_body(const DSParams& p, float* W, int blk
     for (int i = threadIdx.x * 4; i < nstage; i += DS_BLOCK * 4)
         *reinterpret_cast<float4*>(W + i) = *reinterpret_cast<const float4*>(src + i);
     __syncthreads();
-    float* xs = VG ? W + VG_FLOATS + (threadIdx.x >> 6) * VG_SCRATCH : nullptr;
+    float* xs = VG ? W + VG_FLOATS + (threadIdx.x >> 6) * P * VG_SCRATCH : nullptr;
     const int lane = threadIdx.x & 63;
     // wave-major numbering: a batch of fewer groups than waves puts one wave on each SIMD
     // of every CU (waves 0-3 of a block sit on its 4 SIMDs) before any SIMD takes a second
@@ -665,7 +681,7 @@ __device__ __forceinline__ void ds_fwd_body(const DSParams& p, float* W, int blk
 template <int TS, int P, int MODE>
 __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
     if (MODE == 2 && p.ex_on && ds_dqn_explore(p)) return;  // (uniform: the DQN step explores)
-    __shared__ __attribute__((aligned(16))) float W[DSGeom<TS, P>::LDS];
+    __shared__ __attribute__((aligned(16))) float W[DSGeom<TS, P, MODE>::LDS];
     ds_fwd_body<TS, P, MODE>(p, W, blockIdx.x, gridDim.x);
 }
 

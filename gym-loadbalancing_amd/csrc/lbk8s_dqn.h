@@ -51,7 +51,7 @@ struct DQNReplay {  // lb_replay_add's buffers
 template <int P>
 __global__ __launch_bounds__(DS_BLOCK, 2) void k_dqn_step(DSParams d, Params e, DQNReplay r, int nsteps,
                                                          int32_t* sync) {
-    static_assert(P == 2 || P == 4, "envs per wave iteration");
+    static_assert(P == 1 || P == 2, "envs per wave iteration (the VALU Gamma takes at most two)");
     constexpr int NWB = DS_BLOCK / 64;
     const int64_t t = *d.ex.vstep_in;
     const int64_t pos = *r.pos_in;
@@ -63,13 +63,17 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_dqn_step(DSParams d, Params e, 
         *d.ex.vstep_out = t + 1;
         *r.pos_out = (pos + 1) % r.slots;
     }
-    __shared__ __attribute__((aligned(16))) float W[DS_C1L];  // the Q network's fragments
+    // the Q network's VALU image (the actor part of VG_*: Lambda fragments, row-major Gamma: the
+    // Gamma terms of the P sets of a wave iteration as VALU dot products instead of MFMA tiles
+    // with P of 16 columns used), then each wave's scratch
+    __shared__ __attribute__((aligned(16))) float W[VG_ACTOR + NWB * P * VG_SCRATCH];
     const uint32_t all = nsteps >= 32 ? ~0u : (1u << nsteps) - 1u;
     if (exm != all) {  // (some step is greedy)
-        for (int i = threadIdx.x * 4; i < DS_C1L; i += DS_BLOCK * 4)
-            *reinterpret_cast<float4*>(W + i) = *reinterpret_cast<const float4*>(d.wfrag + i);
+        for (int i = threadIdx.x * 4; i < VG_ACTOR; i += DS_BLOCK * 4)
+            *reinterpret_cast<float4*>(W + i) = *reinterpret_cast<const float4*>(d.wfrag + DS_FLOATS + i);
         __syncthreads();
     }
+    float* xs = W + VG_ACTOR + (threadIdx.x >> 6) * P * VG_SCRATCH;
     const int lane = threadIdx.x & 63;
     // wave-major numbering, as k_deepsets_fwd: fewer groups than waves put one wave per SIMD
     const int64_t wave = (int64_t)(threadIdx.x >> 6) * gridDim.x + blockIdx.x;
@@ -96,7 +100,7 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_dqn_step(DSParams d, Params e, 
             if (!explore) {
                 float h0[P][2], m0[2];
                 ds_group_obs<1, P, 2>(d, env0, col, grp, R, h0, m0);
-                act = ds_group_actor<1, P, 2>(d, W, lane, env0, col, grp, R, h0, m0);
+                act = ds_group_actor<1, P, 2, true>(d, W, lane, env0, col, grp, R, h0, m0, xs);
             }
             const int32_t ag = __shfl(act, s < P ? s : 0);
             // the env step: lanes 16 s .. 16 s + 15 step env env0 + s (k_step_slice<16, 1>'s body,
