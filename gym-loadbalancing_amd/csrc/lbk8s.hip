@@ -907,6 +907,16 @@ void ds_forward_launch(const DSParams& p, hipStream_t s) {
         while (P > 1 && (p.B + P - 1) / P < simds) P /= 2;
     }
     const unsigned grid = ds_grid_spread((p.B + P - 1) / P);
+    if constexpr (MODE == 1) {  // R = 16 TS + 1 (config 4's 65): TS tiles and the extra row (XR)
+        if (p.R == 49) {
+            hipLaunchKernelGGL((k_deepsets_fwd<3, 1, 1, true>), dim3(grid), dim3(DS_BLOCK), 0, s, p);
+            return;
+        }
+        if (p.R == 65) {
+            hipLaunchKernelGGL((k_deepsets_fwd<4, 1, 1, true>), dim3(grid), dim3(DS_BLOCK), 0, s, p);
+            return;
+        }
+    }
     switch (ts) {
         case 1:
             if (P == 4) hipLaunchKernelGGL((k_deepsets_fwd<1, 4, MODE>), dim3(grid), dim3(DS_BLOCK), 0, s, p);

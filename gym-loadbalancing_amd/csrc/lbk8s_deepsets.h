@@ -95,24 +95,47 @@ constexpr int DS_LDS_FLOATS = DS_FLOATS;  // 132 KiB of weight fragments: one bl
 // row-major weights, padded rows (stride 68 / 12 floats: a 16-lane ds_read_b128 group covers the
 // 64 banks once).  The set-wise Lambda terms stay on MFMA (their fragments are copied here so the
 // image is one contiguous LDS stage).  Gamma matrices are stored negated, as the fragments.
+// The actor's last layer (64 -> 1) is two plain 64-vectors (A3V: Lambda3, A3GV: -Gamma3).
+// Regions in stage order: the actor's, the critic's, rho's, then the extra-row block (XR, the
+// training forward of R = 16 TS + 1 elements, below: the four layers' Lambda row-major).
 enum : int {
     VG_RS = 68, VG_RS8 = 12,
-    VG_A1L = 0, VG_A2L = 512, VG_A3L = 4608, VG_A3G = 5632, VG_A1G = 6656, VG_A2G = 7424, VG_ACTOR = 11776,
-    VG_C1L = 11776, VG_C2L = 12288, VG_C1G = 16384, VG_C2G = 17152, VG_C3L = 21504, VG_C3G = 25856,
-    VG_R1W = 30208, VG_R1B = 34560, VG_R2W = 34624, VG_R2B = 34688, VG_FLOATS = 34692,
+    VG_A1L = 0, VG_A2L = 512, VG_A3V = 4608, VG_A3GV = 4672, VG_A1G = 4736, VG_A2G = 5504, VG_ACTOR = 9856,
+    VG_C1L = 9856, VG_C2L = 10368, VG_C1G = 14464, VG_C2G = 15232, VG_C3L = 19584, VG_C3G = 23936,
+    VG_CRITIC = 28288,
+    VG_R1W = 28288, VG_R1B = 32640, VG_R2W = 32704, VG_R2B = 32768, VG_RHO = 32772,
+    VG_XA1 = 32772, VG_XA2 = 33540, VG_XC1 = 37892, VG_XC2 = 38660, VG_FLOATS = 43012,
     DS_IMG_FLOATS = DS_FLOATS + VG_FLOATS,
     VG_SCRATCH = 128,  // per wave and env of a wave iteration: the matvec input x[64] and output y[64]
+    // the XR forward's LDS: the actor and critic regions, then the extra-row block
+    VGX_BASE = VG_CRITIC, VGX_A1 = VGX_BASE, VGX_A2 = VGX_BASE + (VG_XA2 - VG_XA1),
+    VGX_C1 = VGX_BASE + (VG_XC1 - VG_XA1), VGX_C2 = VGX_BASE + (VG_XC2 - VG_XA1),
+    VGX_END = VGX_BASE + (VG_FLOATS - VG_XA1),
 };
 // VG: the forwards with one env per wave iteration and >= 3 set tiles, and the greedy-action
 // forward (MODE 2: the DQN's Q values) of small sets with one or two envs per iteration -- the
-// same arithmetic as k_dqn_step's Q forward, so lb_dqn_act and lb_dqn_step pick the same actions
-template <int TS, int P, int MODE = 0>
+// same arithmetic as k_dqn_step's Q forward, so lb_dqn_act and lb_dqn_step pick the same actions.
+// XR: the training forward (MODE 1, VG) of R = 16 TS + 1 set elements (config 4's R = 65: E = 64
+// servers and the reject row).  The TS full tiles run as above; the one extra row -- a fifth
+// 16-row tile with one live column, 20% of the forward's MFMA issue -- is VALU dot products per
+// layer (lane f: output feature f), its outputs folded into the set-wise maxima, argmax rows and
+// the psi sum as a last row.
+template <int TS, int P, int MODE = 0, bool XR = false>
 struct DSGeom {
     static constexpr bool VG = (TS >= 3 && P == 1) || (MODE == 2 && TS == 1 && P <= 2);
-    static constexpr int LDS = VG ? VG_FLOATS + (DS_BLOCK / 64) * P * VG_SCRATCH : DS_LDS_FLOATS;
+    static_assert(!XR || (VG && MODE == 1 && P == 1), "the extra row: one-env VALU-image training forward");
+    static constexpr int IMG = XR ? VGX_END : (MODE == 1 ? VG_CRITIC : VG_RHO);
+    static constexpr int LDS = VG ? IMG + (DS_BLOCK / 64) * P * VG_SCRATCH : DS_LDS_FLOATS;
 };
+static_assert(DSGeom<4, 1, 1, true>::LDS * 4 <= 160 * 1024, "XR forward LDS");
 // (wave-local LDS ordering: the wave's own writes before its later reads by other lanes)
 __device__ __forceinline__ void ds_wave_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// ELU(alpha=1) without a divergent branch: exp2 on the clamped argument
+__device__ __forceinline__ float act_elu(float x) {
+    const float e = __builtin_amdgcn_exp2f(fminf(x, 0.f) * 1.4426950408889634f) - 1.0f;
+    return x > 0.f ? x : e;
+}
+__device__ __forceinline__ float act_relu(float x) { return x > 0.f ? x : 0.f; }
 // the set's max (lane (col, grp) holds env col mod P's, feature in(k, grp)) into x[KS * 4]
 // (P envs: env s's at x + 128 s, written by the lanes of column s)
 template <int KS>
@@ -148,14 +171,57 @@ __device__ __forceinline__ float vg_dot(const float* Wrm, const float* x, int la
 // (-Gamma) max_set(h) of each of the P envs by VALU into the scratch: y_s = xs + 128 s + 64.
 // Lane f computes output f of every env (P dot products); the caller reads the accumulator
 // layout, y_s[16 nt + 4 grp + i], where it initialises the accumulators (vg_init)
+// (returns env 0's output f = lane: the XR forward's extra row starts from it)
 template <int KS, int P>
-__device__ __forceinline__ void vg_gamma(const float* Grm, const float (&mb)[KS], float* xs, int lane) {
+__device__ __forceinline__ float vg_gamma(const float* Grm, const float (&mb)[KS], float* xs, int lane) {
     const int col = lane & 15, grp = lane >> 4;
     vg_put<KS>(mb, xs, col, grp, P);
     ds_wave_fence();
+    float y0 = 0.f;
 #pragma unroll
-    for (int s = 0; s < P; ++s)
-        xs[128 * s + 64 + lane] = vg_dot<4 * KS, KS == 2 ? VG_RS8 : VG_RS>(Grm, xs + 128 * s, lane, 0.f);
+    for (int s = 0; s < P; ++s) {
+        const float y = vg_dot<4 * KS, KS == 2 ? VG_RS8 : VG_RS>(Grm, xs + 128 * s, lane, 0.f);
+        xs[128 * s + 64 + lane] = y;
+        if (s == 0) y0 = y;
+    }
+    ds_wave_fence();
+    return y0;
+}
+// XR: the extra row's layer output for feature f = lane, act(Lambda x + (-Gamma) max_set(h)):
+// g the Gamma term (vg_gamma), x the row's layer input -- the observation row (KS = 2: lane
+// (col, grp) holds features 4kk + grp, put by the column-0 lanes) or the previous layer's
+// extra-row output (KS = 16: lane f holds feature f).  Accumulates Gamma first, then the inputs
+// in order, as the tiles' chains.  The scratch's earlier reads have completed (eq_layer fences).
+template <int KS, int ACT>
+__device__ __forceinline__ float vg_xrow(const float* Lrm, const float* x2, float x64, float g, float* xs, int lane) {
+    if constexpr (KS == 2) {
+        const int col = lane & 15, grp = lane >> 4;
+        if (col == 0) {
+            xs[grp] = x2[0];
+            xs[4 + grp] = x2[1];
+        }
+    } else {
+        xs[lane] = x64;
+    }
+    ds_wave_fence();
+    const float z = vg_dot<4 * KS, KS == 2 ? VG_RS8 : VG_RS>(Lrm, xs, lane, g);
+    ds_wave_fence();
+    return ACT == 1 ? act_relu(z) : act_elu(z);
+}
+// the extra row's output (lane f: feature f) in the accumulator layout: xr[k] = feature
+// 16 (k >> 2) + 4 grp + (k & 3), the tiles' layout of this lane's row group
+__device__ __forceinline__ void vg_xspread(float v, float* xs, int lane, float (&xr)[16]) {
+    const int grp = lane >> 4;
+    xs[lane] = v;
+    ds_wave_fence();
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const float4 q = *reinterpret_cast<const float4*>(xs + 16 * t + 4 * grp);
+        xr[4 * t] = q.x;
+        xr[4 * t + 1] = q.y;
+        xr[4 * t + 2] = q.z;
+        xr[4 * t + 3] = q.w;
+    }
     ds_wave_fence();
 }
 __device__ __forceinline__ dsf4 vg_init(const float* xs, int s, int nt, int grp) {
@@ -221,13 +287,6 @@ __device__ __forceinline__ float from_col_dyn(float v, int s) {
     }
 }
 
-// ELU(alpha=1) without a divergent branch: exp2 on the clamped argument
-__device__ __forceinline__ float act_elu(float x) {
-    const float e = __builtin_amdgcn_exp2f(fminf(x, 0.f) * 1.4426950408889634f) - 1.0f;
-    return x > 0.f ? x : e;
-}
-__device__ __forceinline__ float act_relu(float x) { return x > 0.f ? x : 0.f; }
-
 // A wave iteration holds P envs of TS set tiles each: fragment array h[P*TS][KS], tile
 // (s, t) = env s, set elements 16t..16t+15.  Per-env reductions (max, mean) run over that
 // env's valid columns; the Gamma pass and rho are BATCHED over the P envs: column c of their
@@ -275,9 +334,12 @@ __device__ __forceinline__ void store_obs_max(const float (&mb)[2], int col, int
 // its max over its rows and the first row attaining it (strict > over ascending tiles);
 // the set's max is the 16 columns' max, its first row the smallest row among the lanes
 // holding it.  Both go to setvec (lane col == s stores env s), the batched max to mb.
+// XR (xr non-null, P = 1): the extra row R - 1, after every tile row, in the accumulator
+// layout; it is the max where strictly greater
 template <int TS, int P, int KS>
 __device__ __forceinline__ void set_max_store(const float (&h)[P * TS][KS], float (&mb)[KS], int col, int grp, int R,
-                                              int64_t env0, int64_t B, float* setvec, int off_max, int off_id) {
+                                              int64_t env0, int64_t B, float* setvec, int off_max, int off_id,
+                                              const float* xr = nullptr) {
     static_assert(KS == 16, "hidden layers");
     float m[KS * P], rr[KS * P];
 #pragma unroll
@@ -302,6 +364,14 @@ __device__ __forceinline__ void set_max_store(const float (&h)[P * TS][KS], floa
 #pragma unroll
     for (int i = 0; i < KS * P; ++i) m[i] = m[i] == M[i] ? -rr[i] : -1e9f;
     row_reduce<true>(m);  // -(first row)
+    if (xr) {
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+            const bool u = xr[k] > M[k];
+            M[k] = u ? xr[k] : M[k];
+            m[k] = u ? -(float)(R - 1) : m[k];
+        }
+    }
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
         float r = M[k * P];
@@ -332,16 +402,18 @@ __device__ __forceinline__ void set_max_store(const float (&h)[P * TS][KS], floa
 // at a time left the DPP broadcast of each Gamma result on the critical path).  Every
 // element still accumulates Gamma first, then k = 0..KS-1 in order: the same bits.
 // VG (DSGeom<TS, P>::VG): G is the row-major Gamma of the VALU image and xs the wave's scratch;
-// the Gamma term is then vg_gamma's instead of 4 x KS MFMAs with one useful column
+// the Gamma term is then vg_gamma's instead of 4 x KS MFMAs with one useful column (gret: env 0's
+// Gamma term of output feature lane, for the XR forward's extra row)
 template <int TS, int P, int KS, int ACT, bool VG = false>
 __device__ __forceinline__ void eq_layer(const float* L, const float* G, const float (&h)[P * TS][KS],
                                          const float (&mb)[KS], float (&out)[P * TS][16], int lane,
-                                         float* xs = nullptr) {
+                                         float* xs = nullptr, float* gret = nullptr) {
     constexpr int ST = P * TS;
     dsf4 g[4];  // (MFMA: env s's result in column s; VG: in the scratch, every lane reads its part)
     if constexpr (VG) {
         static_assert(P <= 2, "VALU Gamma: one or two envs per wave iteration");
-        vg_gamma<KS, P>(G, mb, xs, lane);
+        const float g0 = vg_gamma<KS, P>(G, mb, xs, lane);
+        if (gret) *gret = g0;
     } else {
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) g[nt] = dsf4{0.f, 0.f, 0.f, 0.f};
@@ -420,10 +492,16 @@ __device__ __forceinline__ void store_rows(float* plane, const float (&h)[P * TS
         }
 }
 
+// XR training forward: the extra row's layer output (lane f: feature f) to row R - 1 of the plane
+__device__ __forceinline__ void store_xrow(float* plane, float v, int64_t env, int64_t B, int R, int lane) {
+    if (env < B) __builtin_nontemporal_store(v, plane + (env * (int64_t)R + R - 1) * 64 + lane);
+}
+
 // one wave iteration's P envs: the observation -> layer-1 B fragments and its set-wise max
-template <int TS, int P, int MODE>
+// (XR: the extra row R - 1 = 16 TS into xr0, features 4kk + grp, and into the max)
+template <int TS, int P, int MODE, bool XR = false>
 __device__ __forceinline__ void ds_group_obs(const DSParams& p, int64_t env0, int col, int grp, int R,
-                                             float (&h0)[P * TS][2], float (&m0)[2]) {
+                                             float (&h0)[P * TS][2], float (&m0)[2], float (&xr0)[2]) {
     constexpr bool TRAIN = MODE == 1;
     // obs -> layer-1 B fragments: k-step kk holds feature 4kk + grp of set element col
 #pragma unroll
@@ -438,41 +516,74 @@ __device__ __forceinline__ void ds_group_obs(const DSParams& p, int64_t env0, in
         }
     }
     set_max_batched<TS, P, 2>(h0, m0, col, R);
+    if constexpr (XR) {
+        const float* x = p.obs + (env0 * (int64_t)R + 16 * TS) * 8;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            xr0[kk] = env0 < p.B ? x[4 * kk + grp] : 0.f;
+            m0[kk] = max2(m0[kk], xr0[kk]);
+        }
+    }
     if (TRAIN) store_obs_max<TS, P>(m0, col, grp, env0, p.B, p.setvec);
 }
 
 // one wave iteration's P envs: the actor (or Q network) Eq(8->64) ReLU Eq(64->64) ELU Eq(64->1);
 // logits / training rows / the masked greedy action (ARGMAX: lane s < P returns env0 + s's)
 // (W: the fragment image, or the VALU image with xs the wave's scratch: DSGeom<TS, P>::VG)
-template <int TS, int P, int MODE, bool VG = DSGeom<TS, P, MODE>::VG>
+template <int TS, int P, int MODE, bool VG = DSGeom<TS, P, MODE>::VG, bool XR = false>
 __device__ __forceinline__ int32_t ds_group_actor(const DSParams& p, const float* W, int lane, int64_t env0, int col,
                                                   int grp, int R, const float (&h0)[P * TS][2], const float (&m0)[2],
-                                                  float* xs = nullptr) {
+                                                  float* xs = nullptr, const float* xr0 = nullptr) {
     constexpr bool TRAIN = MODE == 1, ARGMAX = MODE == 2;
     constexpr int A1L = VG ? VG_A1L : DS_A1L, A1G = VG ? VG_A1G : DS_A1G, A2L = VG ? VG_A2L : DS_A2L,
-                  A2G = VG ? VG_A2G : DS_A2G, A3L = VG ? VG_A3L : DS_A3L, A3G = VG ? VG_A3G : DS_A3G;
+                  A2G = VG ? VG_A2G : DS_A2G;
     int32_t act = -1;
     float h1[P * TS][16], m1[16], h2[P * TS][16], m2[16];
     // ---- actor: Eq(8->64) ReLU Eq(64->64) ELU Eq(64->1)
     if (p.actor) {
-        eq_layer<TS, P, 2, 1, VG>(W + A1L, W + A1G, h0, m0, h1, lane, xs);
+        float g = 0.f, r1 = 0.f, r2 = 0.f, xr[16];  // (XR: the extra row, below)
+        eq_layer<TS, P, 2, 1, VG>(W + A1L, W + A1G, h0, m0, h1, lane, xs, XR ? &g : nullptr);
+        if constexpr (XR) {
+            r1 = vg_xrow<2, 1>(W + VGX_A1, xr0, 0.f, g, xs, lane);
+            vg_xspread(r1, xs, lane, xr);
+            store_xrow(p.save_actor, r1, env0, p.B, R, lane);
+        }
         if (TRAIN) store_rows<TS, P>(p.save_actor, h1, env0, p.B, R, col, grp);
-        if (TRAIN) set_max_store<TS, P, 16>(h1, m1, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX1A, LB_DSV_ID1A);
+        if (TRAIN)
+            set_max_store<TS, P, 16>(h1, m1, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX1A, LB_DSV_ID1A,
+                                     XR ? xr : nullptr);
         else set_max_batched<TS, P, 16>(h1, m1, col, R);
-        eq_layer<TS, P, 16, 2, VG>(W + A2L, W + A2G, h1, m1, h2, lane, xs);
+        eq_layer<TS, P, 16, 2, VG>(W + A2L, W + A2G, h1, m1, h2, lane, xs, XR ? &g : nullptr);
+        if constexpr (XR) {
+            r2 = vg_xrow<16, 2>(W + VGX_A2, nullptr, r1, g, xs, lane);
+            vg_xspread(r2, xs, lane, xr);
+            store_xrow(p.save_actor + p.B * (int64_t)R * 64, r2, env0, p.B, R, lane);
+        }
         if (TRAIN) store_rows<TS, P>(p.save_actor + p.B * (int64_t)R * 64, h2, env0, p.B, R, col, grp);
-        if (TRAIN) set_max_store<TS, P, 16>(h2, m2, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX2A, LB_DSV_ID2A);
+        if (TRAIN)
+            set_max_store<TS, P, 16>(h2, m2, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX2A, LB_DSV_ID2A,
+                                     XR ? xr : nullptr);
         else set_max_batched<TS, P, 16>(h2, m2, col, R);
         // layer 3 (64 -> 1) on the VALU: a 16-row output tile would use 1/16 of an MFMA.
-        // Lane (col, grp) dots its 16 features with Lambda3 / -Gamma3 (row 0 of the
-        // fragments: column 0 of its row group), then the 4 row groups are summed.
-        const float* L = W + A3L + 16 * grp;
-        const float* G = W + A3G + 16 * grp;
+        // Lane (col, grp) dots its 16 features in(k, grp) with Lambda3 / -Gamma3 (the VALU
+        // image's vectors, or row 0 of the fragments: column 0 of its row group), then the 4
+        // row groups are summed.
+        auto l3 = [&](int k, bool gamma) {
+            return VG ? W[(gamma ? VG_A3GV : VG_A3V) + 16 * (k >> 2) + 4 * grp + (k & 3)]
+                      : W[(gamma ? DS_A3G : DS_A3L) + 16 * grp + 64 * k];
+        };
         float gl = 0.f;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) gl += G[k * 64] * m2[k];
+        for (int k = 0; k < 16; ++k) gl += l3(k, true) * m2[k];
         gl += __shfl_xor(gl, 16);
         gl += __shfl_xor(gl, 32);
+        if constexpr (XR) {  // the extra row's logit: lane f's product, summed over the wave
+            float v[1] = {W[VG_A3V + lane] * r2};
+            row_reduce<false>(v);
+            v[0] += __shfl_xor(v[0], 16);
+            v[0] += __shfl_xor(v[0], 32);
+            if (lane == 0 && env0 < p.B && p.logits) p.logits[env0 * R + R - 1] = gl + v[0];
+        }
         float best[P], brow[P];  // this lane's first masked maximum per env (argmax mode)
 #pragma unroll
         for (int s = 0; s < P; ++s) {
@@ -483,7 +594,7 @@ __device__ __forceinline__ int32_t ds_group_actor(const DSParams& p, const float
             for (int t = 0; t < TS; ++t) {
                 float v = 0.f;
 #pragma unroll
-                for (int k = 0; k < 16; ++k) v += L[k * 64] * h2[s * TS + t][k];
+                for (int k = 0; k < 16; ++k) v += l3(k, false) * h2[s * TS + t][k];
                 v += __shfl_xor(v, 16);
                 v += __shfl_xor(v, 32);
                 const int row = 16 * t + col;
@@ -523,18 +634,22 @@ __device__ __forceinline__ int32_t ds_group_actor(const DSParams& p, const float
 // and the masked greedy action (ARGMAX; actor only)
 // the forward of the blocks blk = 0 .. nblk - 1 (k_deepsets_fwd: the whole grid; k_ds_fwd_pair:
 // its half of the grid), W the block's LDS weight region
-template <int TS, int P, int MODE>
+template <int TS, int P, int MODE, bool XR = false>
 __device__ __forceinline__ void ds_fwd_body(const DSParams& p, float* W, int blk, int nblk) {
-    constexpr bool TRAIN = MODE == 1, ARGMAX = MODE == 2, VG = DSGeom<TS, P, MODE>::VG;
+    constexpr bool TRAIN = MODE == 1, ARGMAX = MODE == 2, VG = DSGeom<TS, P, MODE, XR>::VG;
     // stage the weight image (once per block; blocks are persistent): the fragment image, or
-    // the VALU image (VG); an actor-only launch (DQN) stages only the actor's part
-    const int nstage = VG ? ((ARGMAX || !p.critic) ? (int)VG_ACTOR : (int)VG_FLOATS)
+    // the VALU image (VG: the actor's and critic's regions, rho's for the inference forward, the
+    // extra-row block for XR); an actor-only launch (DQN) stages only the actor's part
+    const int nstage = VG ? ((ARGMAX || !p.critic) ? (int)VG_ACTOR : (int)DSGeom<TS, P, MODE>::IMG)
                           : ((ARGMAX || !p.critic) ? (int)DS_C1L : (int)DS_FLOATS);
     const float* src = p.wfrag + (VG ? DS_FLOATS : 0);
     for (int i = threadIdx.x * 4; i < nstage; i += DS_BLOCK * 4)
         *reinterpret_cast<float4*>(W + i) = *reinterpret_cast<const float4*>(src + i);
+    if constexpr (XR)
+        for (int i = threadIdx.x * 4; i < VG_FLOATS - VG_XA1; i += DS_BLOCK * 4)
+            *reinterpret_cast<float4*>(W + VGX_BASE + i) = *reinterpret_cast<const float4*>(src + VG_XA1 + i);
     __syncthreads();
-    float* xs = VG ? W + VG_FLOATS + (threadIdx.x >> 6) * P * VG_SCRATCH : nullptr;
+    float* xs = VG ? W + DSGeom<TS, P, MODE, XR>::IMG + (threadIdx.x >> 6) * P * VG_SCRATCH : nullptr;
     const int lane = threadIdx.x & 63;
     // wave-major numbering: a batch of fewer groups than waves puts one wave on each SIMD
     // of every CU (waves 0-3 of a block sit on its 4 SIMDs) before any SIMD takes a second
@@ -545,22 +660,37 @@ __device__ __forceinline__ void ds_fwd_body(const DSParams& p, float* W, int blk
     const int64_t groups = (p.B + P - 1) / P;
     for (int64_t gi = wave; gi < groups; gi += nwaves) {
         const int64_t env0 = gi * P;
-        float h0[P * TS][2], m0[2];
-        ds_group_obs<TS, P, MODE>(p, env0, col, grp, R, h0, m0);
-        ds_group_actor<TS, P, MODE>(p, W, lane, env0, col, grp, R, h0, m0, xs);
+        float h0[P * TS][2], m0[2], xr0[2];
+        ds_group_obs<TS, P, MODE, XR>(p, env0, col, grp, R, h0, m0, xr0);
+        ds_group_actor<TS, P, MODE, VG, XR>(p, W, lane, env0, col, grp, R, h0, m0, xs, xr0);
         float h1[P * TS][16], m1[16], h2[P * TS][16], m2[16];
         if (ARGMAX || !p.critic) continue;
 
         // ---- critic: psi = Eq ELU Eq ELU Eq, mean over the set, rho = Linear ELU Linear
         constexpr int C1L = VG ? VG_C1L : DS_C1L, C1G = VG ? VG_C1G : DS_C1G, C2L = VG ? VG_C2L : DS_C2L,
                       C2G = VG ? VG_C2G : DS_C2G;
-        eq_layer<TS, P, 2, 2, VG>(W + C1L, W + C1G, h0, m0, h1, lane, xs);
+        float g = 0.f, c1r = 0.f, xr[16];  // (XR: the extra row, as the actor's)
+        eq_layer<TS, P, 2, 2, VG>(W + C1L, W + C1G, h0, m0, h1, lane, xs, XR ? &g : nullptr);
+        if constexpr (XR) {
+            c1r = vg_xrow<2, 2>(W + VGX_C1, xr0, 0.f, g, xs, lane);
+            vg_xspread(c1r, xs, lane, xr);
+            store_xrow(p.save_critic, c1r, env0, p.B, R, lane);
+        }
         if (TRAIN) store_rows<TS, P>(p.save_critic, h1, env0, p.B, R, col, grp);
-        if (TRAIN) set_max_store<TS, P, 16>(h1, m1, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX1C, LB_DSV_ID1C);
+        if (TRAIN)
+            set_max_store<TS, P, 16>(h1, m1, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX1C, LB_DSV_ID1C,
+                                     XR ? xr : nullptr);
         else set_max_batched<TS, P, 16>(h1, m1, col, R);
-        eq_layer<TS, P, 16, 2, VG>(W + C2L, W + C2G, h1, m1, h2, lane, xs);
+        eq_layer<TS, P, 16, 2, VG>(W + C2L, W + C2G, h1, m1, h2, lane, xs, XR ? &g : nullptr);
+        if constexpr (XR) {
+            const float c2r = vg_xrow<16, 2>(W + VGX_C2, nullptr, c1r, g, xs, lane);
+            vg_xspread(c2r, xs, lane, xr);  // (xr: c2's extra row, into the max and the sum)
+            store_xrow(p.save_critic + p.B * (int64_t)R * 64, c2r, env0, p.B, R, lane);
+        }
         if (TRAIN) store_rows<TS, P>(p.save_critic + p.B * (int64_t)R * 64, h2, env0, p.B, R, col, grp);
-        if (TRAIN) set_max_store<TS, P, 16>(h2, m2, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX2C, LB_DSV_ID2C);
+        if (TRAIN)
+            set_max_store<TS, P, 16>(h2, m2, col, grp, R, env0, p.B, p.setvec, LB_DSV_MAX2C, LB_DSV_ID2C,
+                                     XR ? xr : nullptr);
         else set_max_batched<TS, P, 16>(h2, m2, col, R);
         // layer 3 has no activation and only its mean over the set is used, so
         // mean_r(Lambda3 c2[r] - Gamma3 max(c2)) = Lambda3 mean_r(c2) - Gamma3 max(c2): one
@@ -577,6 +707,10 @@ __device__ __forceinline__ void ds_fwd_body(const DSParams& p, float* W, int blk
                 sm[k] = v;
             }
             row_reduce<false>(sm);
+            if constexpr (XR) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) sm[k] += xr[k];
+            }
             const float invR = 1.0f / (float)R;
 #pragma unroll
             for (int k = 0; k < 16; ++k) sm[k] *= invR;
@@ -678,11 +812,11 @@ __device__ __forceinline__ void ds_fwd_body(const DSParams& p, float* W, int blk
     }
 }
 
-template <int TS, int P, int MODE>
+template <int TS, int P, int MODE, bool XR = false>
 __global__ __launch_bounds__(DS_BLOCK, 2) void k_deepsets_fwd(DSParams p) {
     if (MODE == 2 && p.ex_on && ds_dqn_explore(p)) return;  // (uniform: the DQN step explores)
-    __shared__ __attribute__((aligned(16))) float W[DSGeom<TS, P, MODE>::LDS];
-    ds_fwd_body<TS, P, MODE>(p, W, blockIdx.x, gridDim.x);
+    __shared__ __attribute__((aligned(16))) float W[DSGeom<TS, P, MODE, XR>::LDS];
+    ds_fwd_body<TS, P, MODE, XR>(p, W, blockIdx.x, gridDim.x);
 }
 
 // two forwards in one launch (lb_ds_forward_pair: the DQN train step's target-network Q values
@@ -990,17 +1124,17 @@ __device__ __forceinline__ float vg_rm_value(const float* w, int kin, int S, int
     return (w && j < kin) ? w[f * kin + j] : 0.f;
 }
 __device__ __forceinline__ void vg_pack_one(const lb_ds_weights& w, float* out, int j) {
-    const int starts[16] = {VG_A1L, VG_A2L, VG_A3L, VG_A3G, VG_A1G, VG_A2G, VG_C1L, VG_C2L,
-                            VG_C1G, VG_C2G, VG_C3L, VG_C3G, VG_R1W, VG_R1B, VG_R2W, VG_R2B};
-    int r = 15;
+    const int starts[20] = {VG_A1L, VG_A2L, VG_A3V, VG_A3GV, VG_A1G, VG_A2G, VG_C1L, VG_C2L, VG_C1G, VG_C2G,
+                            VG_C3L, VG_C3G, VG_R1W, VG_R1B, VG_R2W, VG_R2B, VG_XA1, VG_XA2, VG_XC1, VG_XC2};
+    int r = 19;
     while (r > 0 && j < starts[r]) --r;
     const int idx = j - starts[r];
     float v = 0.f;
     switch (r) {
         case 0: v = ds_frag_value(w.actor_lambda[0], 64, 8, 2, idx); break;
         case 1: v = ds_frag_value(w.actor_lambda[1], 64, 64, 16, idx); break;
-        case 2: v = ds_frag_value(w.actor_lambda[2], 1, 64, 16, idx); break;
-        case 3: v = -ds_frag_value(w.actor_gamma[2], 1, 64, 16, idx); break;
+        case 2: v = w.actor_lambda[2] ? w.actor_lambda[2][idx] : 0.f; break;
+        case 3: v = w.actor_gamma[2] ? -w.actor_gamma[2][idx] : 0.f; break;
         case 4: v = -vg_rm_value(w.actor_gamma[0], 8, VG_RS8, idx); break;
         case 5: v = -vg_rm_value(w.actor_gamma[1], 64, VG_RS, idx); break;
         case 6: v = ds_frag_value(w.critic_lambda[0], 64, 8, 2, idx); break;
@@ -1012,7 +1146,11 @@ __device__ __forceinline__ void vg_pack_one(const lb_ds_weights& w, float* out, 
         case 12: v = vg_rm_value(w.rho_w1, 64, VG_RS, idx); break;
         case 13: v = w.rho_b1 ? w.rho_b1[idx] : 0.f; break;
         case 14: v = w.rho_w2 ? w.rho_w2[idx] : 0.f; break;
-        default: v = (w.rho_b2 && idx == 0) ? w.rho_b2[0] : 0.f; break;
+        case 15: v = (w.rho_b2 && idx == 0) ? w.rho_b2[0] : 0.f; break;
+        case 16: v = vg_rm_value(w.actor_lambda[0], 8, VG_RS8, idx); break;
+        case 17: v = vg_rm_value(w.actor_lambda[1], 64, VG_RS, idx); break;
+        case 18: v = vg_rm_value(w.critic_lambda[0], 8, VG_RS8, idx); break;
+        default: v = vg_rm_value(w.critic_lambda[1], 64, VG_RS, idx); break;
     }
     out[DS_FLOATS + j] = v;
 }

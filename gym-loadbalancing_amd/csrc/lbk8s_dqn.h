@@ -99,7 +99,8 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_dqn_step(DSParams d, Params e, 
             int32_t act = -1;
             if (!explore) {
                 float h0[P][2], m0[2];
-                ds_group_obs<1, P, 2>(d, env0, col, grp, R, h0, m0);
+                float xr0[2];
+                ds_group_obs<1, P, 2>(d, env0, col, grp, R, h0, m0, xr0);
                 act = ds_group_actor<1, P, 2, true>(d, W, lane, env0, col, grp, R, h0, m0, xs);
             }
             const int32_t ag = __shfl(act, s < P ? s : 0);

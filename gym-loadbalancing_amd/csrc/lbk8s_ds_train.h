@@ -229,6 +229,7 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
     float* cv = CV[wv];
     const int R = p.R, ntl = (R + 15) / 16;
     const int nct = ((R - 1) % 16) / 4 + 1;  // 4-row groups of the last tile that hold set rows
+    const bool one_row = R % 16 == 1;        // the last tile holds one set row (below)
     const int col = lane & 15, grp = lane >> 4;
     const int64_t plane = p.B * (int64_t)R * 64;
     const float* in1 = HEAD == 0 ? p.save_actor : p.save_critic;  // h1 / c1
@@ -360,11 +361,12 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
             // the tile through LDS into the data gradient's k layout (row = col): float4 q of
             // row rho at rho * 16 + (q ^ rho), conflict-free both ways
             float4* T4 = reinterpret_cast<float4*>(la);
+            if (!(one_row && t == ntl - 1))
 #pragma unroll
-            for (int cc = 0; cc < 4; ++cc) {
-                const int rho = 4 * cc + grp;
-                T4[rho * 16 + (col ^ rho)] = dz[cc];
-            }
+                for (int cc = 0; cc < 4; ++cc) {
+                    const int rho = 4 * cc + grp;
+                    T4[rho * 16 + (col ^ rho)] = dz[cc];
+                }
             // dLambda2 += dz2^T h1 straight from registers (W layout = the MFMA operands)
 #pragma unroll
             for (int cs = 0; cs < 4; ++cs) {
@@ -376,6 +378,42 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
 #pragma unroll
                     for (int nt = 0; nt < 4; ++nt) w2[mt][nt] = mfma4(av[mt], bv[nt], w2[mt][nt]);
             }
+            float4 pre1 = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (one_row && t == ntl - 1) {
+                // a last tile holding one set row (R = 16 t + 1: config 4's 65), row 16 t on the
+                // lanes of row group 0: its dz2 Lambda2 as lane dot products -- lane (col, grp)
+                // sums inputs 16kq + 4grp + kk of outputs 16nt + col from the same Lambda2^T
+                // fragments, the four row groups added -- instead of 64 MFMAs on one live row
+                float* v = la + 1024;  // (past the transpose's 256 float4)
+                if (grp == 0) *reinterpret_cast<float4*>(v + 4 * col) = dz[0];
+                float dv[16];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 d = *reinterpret_cast<const float4*>(v + 16 * q + 4 * grp);
+                    dv[4 * q] = d.x;
+                    dv[4 * q + 1] = d.y;
+                    dv[4 * q + 2] = d.z;
+                    dv[4 * q + 3] = d.w;
+                }
+                float po[4];
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt) {
+                    float a = 0.f;
+#pragma unroll
+                    for (int kq = 0; kq < 4; ++kq) {
+                        const float4 l = *reinterpret_cast<const float4*>(LTt + ((nt * 4 + kq) * 64 + lane) * 4);
+                        a += l.x * dv[4 * kq] + l.y * dv[4 * kq + 1] + l.z * dv[4 * kq + 2] + l.w * dv[4 * kq + 3];
+                    }
+                    a += __shfl_xor(a, 16);
+                    po[nt] = a + __shfl_xor(a, 32);
+                }
+                // to the W layout (features 4col .. 4col + 3 on row group 0)
+                if (grp == 0)
+#pragma unroll
+                    for (int nt = 0; nt < 4; ++nt) v[64 + 16 * nt + col] = po[nt];
+                const float4 q4 = *reinterpret_cast<const float4*>(v + 64 + 4 * col);
+                if (grp == 0) pre1 = q4;
+            } else {
             // dz2 in k layout (lane: row col, features 16q + 4grp .. + 3 at k = 4q ..)
             float dk[16];
 #pragma unroll
@@ -413,12 +451,14 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt)
                 T4[col * 16 + ((4 * nt + grp) ^ col)] = make_float4(eacc[nt][0], eacc[nt][1], eacc[nt][2], eacc[nt][3]);
+            }
             // dz1 = pre act'(h1) (W layout; the pooled term is added per set), its set sum,
             // dLambda1 += dz1^T obs (B columns 8..15 zero)
 #pragma unroll
             for (int cc = 0; cc < 4; ++cc) {
                 const int rho = 4 * cc + grp;
-                const float4 pre = T4[rho * 16 + (col ^ rho)];
+                const float4 pre = (one_row && t == ntl - 1) ? (cc == 0 ? pre1 : make_float4(0.f, 0.f, 0.f, 0.f))
+                                                             : T4[rho * 16 + (col ^ rho)];
                 const float pa[4] = {pre.x, pre.y, pre.z, pre.w};
                 const float ha[4] = {c.h[cc].x, c.h[cc].y, c.h[cc].z, c.h[cc].w};
                 float d1[4];

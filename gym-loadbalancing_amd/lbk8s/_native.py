@@ -16,7 +16,7 @@ CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
 SOURCES = ("lbk8s.hip", "lbk8s_common.h", "lbk8s_slice.h", "lbk8s_tpe.h", "lbk8s_rollout.h", "lbk8s_lean.h",
            "lbk8s_deepsets.h", "lbk8s_ds_train.h", "lbk8s_dqn.h", "../../include/lbk8s.h", "lbk8s_lean_launch.h",
            "lbk8s_lean_inst.hip", "lbk8s_build.cpp")
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 LB_REWARD = {"naive": 0, "latency": 1, "fairness": 2, "multi": 3}
 LB_RNG_PHILOX, LB_RNG_TRACE = 0, 1
@@ -63,7 +63,7 @@ class LBDSWeightsC(C.Structure):
                 ("rho_b2", C.c_void_p)]
 
 
-LB_DS_FRAG_FLOATS = 68552
+LB_DS_FRAG_FLOATS = 76872
 LB_DS_MAX_ELEMENTS = 80       # forward held in registers (above: streamed in chunks)
 LB_DS_MAX_ELEMENTS_TRAIN = 257  # training forward / backward, PPO loss head
 LB_DS_MAX_ELEMENTS_FWD = 257  # inference forward / greedy argmax

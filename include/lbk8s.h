@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LBK8S_ABI_VERSION 12
+#define LBK8S_ABI_VERSION 13
 
 /* reward_function names of loadbalancer_k8s_env.py:20-31 */
 enum { LB_REWARD_NAIVE = 0, LB_REWARD_LATENCY = 1, LB_REWARD_FAIRNESS = 2, LB_REWARD_MULTI = 3 };
@@ -239,7 +239,7 @@ int lb_status(const void* state, const lb_config* cfg, int64_t num_envs, uint32_
  * MFMA fragment order, then (ABI 12) the VALU image of the forwards with 33..80 set elements,
  * row-major matrix-vector weights), to be redone after every optimizer step.  A NULL critic pointer set packs an actor-only
  * image (DQN); lb_ds_forward then must be called with value_out == NULL. */
-#define LB_DS_FRAG_FLOATS 68552
+#define LB_DS_FRAG_FLOATS 76872
 #define LB_DS_MAX_ELEMENTS 80       /* forward held in registers (above: streamed in chunks) */
 #define LB_DS_MAX_ELEMENTS_TRAIN 257 /* training forward / backward, PPO loss head */
 #define LB_DS_MAX_ELEMENTS_FWD 257  /* inference forward, greedy argmax */
