@@ -1250,27 +1250,27 @@ int lb_ds_over_sets(const lb_set_job* jobs, int32_t num_jobs, int64_t num_sets, 
     if (!jobs || num_jobs < 1 || num_jobs > OS_JOBS || num_sets < 1 || !workspace)
         return fail("lb_ds_over_sets: jobs NULL, num_jobs not in [1, 16], num_sets < 1 or workspace NULL");
     OverSetsParams p{};
-    int tiles = 0, row = 0;
+    int row = 0;
+    auto vec_ok = [](const float* x, int64_t ld) { return ((uintptr_t)x & 15) == 0 && ld % 4 == 0; };
     for (int i = 0; i < num_jobs; ++i) {
         const lb_set_job& j = jobs[i];
         if (!j.b || !j.out || j.M < 1 || j.N < 1 || j.M > 64 || j.N > 64 || (!j.a && j.M != 1))
             return fail("lb_ds_over_sets: a job needs b and out, 1 <= M, N <= 64 (M == 1 when a is NULL)");
-        p.job[i] = OverSetsJob{j.a, j.lda, j.b, j.ldb, j.M, j.N, j.scale, j.out, row, tiles};
-        tiles += ((j.M + 15) / 16) * ((j.N + 15) / 16);
+        p.job[i] = OverSetsJob{j.a, j.lda, j.b, j.ldb, j.M, j.N, j.scale, j.out, row,
+                               (vec_ok(j.a, j.lda) ? 1 : 0) | (vec_ok(j.b, j.ldb) ? 2 : 0)};
         row += j.M * j.N;
     }
     p.njobs = num_jobs;
-    p.ntiles = tiles;
     p.row = row;
     p.S = num_sets;
     p.work = workspace;
     const int64_t spans = (num_sets + OS_SPAN - 1) / OS_SPAN;
     if (spans * row > workspace_floats) return fail("lb_ds_over_sets: workspace too small (spans x outputs)");
     if (spans > 65535) return fail("lb_ds_over_sets: num_sets too large");
-    hipLaunchKernelGGL(k_ds_over_sets, dim3((unsigned)((tiles + 3) / 4), (unsigned)spans), dim3(256), 0,
+    hipLaunchKernelGGL(k_ds_over_sets, dim3((unsigned)((num_jobs + 3) / 4), (unsigned)spans), dim3(256), 0,
                        (hipStream_t)stream, p);
     if (int r = check_launch()) return r;
-    hipLaunchKernelGGL(k_ds_over_sets_reduce, dim3((unsigned)((row + 255) / 256)), dim3(256), 0, (hipStream_t)stream, p,
+    hipLaunchKernelGGL(k_ds_over_sets_reduce, dim3((unsigned)((row + 63) / 64)), dim3(64 * OS_RG), 0, (hipStream_t)stream, p,
                        (int)spans);
     return check_launch();
 }

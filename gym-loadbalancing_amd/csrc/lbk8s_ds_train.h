@@ -889,11 +889,14 @@ __global__ __launch_bounds__(SG_THREADS) void k_ds_set_grads(SetGradParams p) {
 // (the PPO minibatch's 51,200), every job in two launches.  The sums over the sets of the
 // training step -- the Gamma gradients (sum_r dz)^T max_set(h), the critic's Lambda3, rho's
 // two weight gradients and the bias sums -- were chunked torch GEMMs plus a reduction each
-// (~20 + 10 us per product: ~0.25 ms per minibatch).  Here one wave owns a 16 x 16 output tile
-// of one job over one span of OS_SPAN sets: v_mfma_f32_16x16x4_f32 with the sets as the K
-// dimension (A operand: lane l holds A(s0 + 4 t + l / 16, 16 mt + l % 16), B: B(s, 16 nt +
-// l % 16)), its partial sums to workspace[span][job output]; k_ds_over_sets_reduce adds the
-// spans in ascending order (deterministic) and scales.
+// (~20 + 10 us per product: ~0.25 ms per minibatch).  Here one wave owns one job's whole output
+// over one span of OS_SPAN sets on v_mfma_f32_16x16x4_f32 with the sets as the K dimension, its
+// partial sums to workspace[span][job output]; k_ds_over_sets_reduce adds the spans in
+// ascending order (deterministic) and scales.
+// Operand layout: a job of M > 16 outputs takes four 16-row tiles i with output m = 4c + i on
+// tile row c, so lane (c, q) reads A(s, 4c .. 4c + 3) of set s = s0 + 4k + q as one float4 and
+// feeds the four tiles (the same for N > 16 and the columns); M, N <= 16: one tile, m = c.
+// A 64 x 64 job: two float4 loads per 16 independent MFMAs, every input read once.
 struct OverSetsJob {
     const float* a;  // A(s, m) = a[s lda + m]; NULL: A(s, 0) = 1 (M == 1: a plain sum of B)
     int64_t lda;
@@ -903,59 +906,121 @@ struct OverSetsJob {
     float scale;
     float* out;      // [M][N]
     int ooff;        // offset of the job's outputs in a span's workspace row
-    int tile0;       // first global tile index of the job (tiles: ceil(M / 16) x ceil(N / 16))
+    int vec;         // bit 0 (1): a (b) 16-byte aligned with lda (ldb) % 4 == 0: float4 operand loads
 };
-constexpr int OS_JOBS = 16, OS_SPAN = 1024;
+constexpr int OS_JOBS = 16, OS_SPAN = LB_DS_OVER_SETS_SPAN, OS_D = 8;
 struct OverSetsParams {
     OverSetsJob job[OS_JOBS];
-    int njobs, ntiles, row;  // row: workspace floats per span (the sum of the jobs' M N)
+    int njobs, row;  // row: workspace floats per span (the sum of the jobs' M N)
     int64_t S;
-    float* work;             // [spans][row]
+    float* work;     // [spans][row]
 };
 
-__global__ __launch_bounds__(256) void k_ds_over_sets(OverSetsParams p) {
-    const int wt = blockIdx.x * 4 + (threadIdx.x >> 6);  // this wave's tile
-    if (wt >= p.ntiles) return;  // (wave-uniform)
-    int ji = 0;
-    while (ji + 1 < p.njobs && wt >= p.job[ji + 1].tile0) ++ji;
-    const OverSetsJob j = p.job[ji];
-    const int t = wt - j.tile0, ntn = (j.N + 15) / 16, mt = t / ntn, nt = t - mt * ntn;
-    const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
-    const int m = 16 * mt + c, n = 16 * nt + c;
-    const int64_t s0 = (int64_t)blockIdx.y * OS_SPAN;
-    const int64_t s1 = s0 + OS_SPAN < p.S ? s0 + OS_SPAN : p.S;
-    dsf4 acc = {0.f, 0.f, 0.f, 0.f};
-    const bool am = m < j.M, bn = n < j.N;
-    const float* ap = j.a ? j.a + m : nullptr;
-    const float* bp = j.b + n;
-    // (a wave-uniform trip count: the MFMA takes every lane; sets past the span's end load 0)
-    const int steps = (int)((s1 - s0 + 3) / 4);
-#pragma unroll 4
-    for (int k = 0; k < steps; ++k) {
-        const int64_t s = s0 + 4 * k + q;
-        const bool in = s < s1;
-        const float av = (am && in) ? (ap ? ap[s * j.lda] : 1.f) : 0.f;
-        const float bv = (bn && in) ? bp[s * j.ldb] : 0.f;
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
-    }
-    float* w = p.work + (int64_t)blockIdx.y * p.row + j.ooff;
+// this lane's operand values of set s for the T tiles (T = 4: outputs 4c .. 4c + 3; T = 1:
+// output c), zero past the job's outputs or the span
+template <int T>
+__device__ __forceinline__ void os_load(const float* p, int64_t ld, int K, bool vec, int c, int64_t s, bool in,
+                                        float (&v)[T]) {
+    if constexpr (T == 4) {
+        if (vec && in && 4 * c + 3 < K) {  // (vec: p 16-byte aligned, ld % 4 == 0)
+            const float4 q = *reinterpret_cast<const float4*>(p + s * ld + 4 * c);
+            v[0] = q.x;
+            v[1] = q.y;
+            v[2] = q.z;
+            v[3] = q.w;
+        } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int mm = 16 * mt + 4 * q + i;
-        if (mm < j.M && bn) w[mm * j.N + n] = acc[i];
+            for (int i = 0; i < 4; ++i) v[i] = (in && 4 * c + i < K) ? p[s * ld + 4 * c + i] : 0.f;
+        }
+    } else {
+        v[0] = (in && c < K) ? (p ? p[s * ld + c] : 1.f) : 0.f;
     }
 }
 
-// out[e] = scale * sum over the spans (ascending) of the partial sums
-__global__ void k_ds_over_sets_reduce(OverSetsParams p, int spans) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= p.row) return;
+template <int MT, int NT>
+__device__ __forceinline__ void os_job(const OverSetsJob& j, int64_t s0, int64_t s1, float* w, int lane) {
+    const int c = lane & 15, q = lane >> 4;
+    dsf4 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[i][t] = dsf4{0.f, 0.f, 0.f, 0.f};
+    // (a wave-uniform trip count: the MFMA takes every lane; sets past the span's end load 0).
+    // The operands of OS_D steps are in flight ahead of the MFMAs (a block holds at most four
+    // jobs' waves, so the latency is hidden in the wave, not by occupancy)
+    const int steps = (int)((s1 - s0 + 3) / 4);
+    float av[OS_D][MT], bv[OS_D][NT];
+#pragma unroll
+    for (int d = 0; d < OS_D; ++d) {
+        const int64_t s = s0 + 4 * d + q;
+        os_load<MT>(j.a, j.lda, j.M, j.vec & 1, c, s, s < s1, av[d]);
+        os_load<NT>(j.b, j.ldb, j.N, j.vec & 2, c, s, s < s1, bv[d]);
+    }
+    for (int k = 0; k < steps; k += OS_D) {
+#pragma unroll
+        for (int d = 0; d < OS_D; ++d) {
+            if (k + d < steps) {
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int t = 0; t < NT; ++t)
+                        acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[d][i], bv[d][t], acc[i][t], 0, 0, 0);
+            }
+            const int64_t s = s0 + 4 * (k + d + OS_D) + q;
+            os_load<MT>(j.a, j.lda, j.M, j.vec & 1, c, s, s < s1, av[d]);
+            os_load<NT>(j.b, j.ldb, j.N, j.vec & 2, c, s, s < s1, bv[d]);
+        }
+    }
+    // tile (i, t) register r of lane (c, q): tile row 4q + r, tile column c
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = MT == 4 ? 4 * (4 * q + r) + i : 4 * q + r, n = NT == 4 ? 4 * c + t : c;
+                if (m < j.M && n < j.N) w[m * j.N + n] = acc[i][t][r];
+            }
+}
+
+__global__ __launch_bounds__(256) void k_ds_over_sets(OverSetsParams p) {
+    const int wj = blockIdx.x * 4 + (threadIdx.x >> 6);  // this wave's job
+    if (wj >= p.njobs) return;                           // (wave-uniform)
+    const OverSetsJob j = p.job[wj];
+    const int64_t s0 = (int64_t)blockIdx.y * OS_SPAN;
+    const int64_t s1 = s0 + OS_SPAN < p.S ? s0 + OS_SPAN : p.S;
+    float* w = p.work + (int64_t)blockIdx.y * p.row + j.ooff;
+    const int lane = threadIdx.x & 63;
+    if (j.M > 16) {
+        if (j.N > 16) os_job<4, 4>(j, s0, s1, w, lane);
+        else os_job<4, 1>(j, s0, s1, w, lane);
+    } else {
+        if (j.N > 16) os_job<1, 4>(j, s0, s1, w, lane);
+        else os_job<1, 1>(j, s0, s1, w, lane);
+    }
+}
+
+// out[e] = scale * sum over the spans of the partial sums: block = 64 outputs x OS_RG span
+// groups (thread (e, g) adds spans g, g + OS_RG, ... in order), the groups combined in LDS in
+// a fixed order (deterministic)
+constexpr int OS_RG = 8;
+__global__ __launch_bounds__(64 * OS_RG) void k_ds_over_sets_reduce(OverSetsParams p, int spans) {
+    __shared__ float part[OS_RG][64];
+    const int o = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int e = blockIdx.x * 64 + o;
+    float acc = 0.f;
+    if (e < p.row)
+        for (int z = g; z < spans; z += OS_RG) acc += p.work[(int64_t)z * p.row + e];
+    part[g][o] = acc;
+    __syncthreads();
+    if (g != 0 || e >= p.row) return;
+    float t = part[0][o];
+#pragma unroll
+    for (int i = 1; i < OS_RG; ++i) t += part[i][o];
     int ji = 0;
     while (ji + 1 < p.njobs && e >= p.job[ji + 1].ooff) ++ji;
     const OverSetsJob& j = p.job[ji];
-    float acc = 0.f;
-    for (int z = 0; z < spans; ++z) acc += p.work[(int64_t)z * p.row + e];
-    j.out[e - j.ooff] = j.scale * acc;
+    j.out[e - j.ooff] = j.scale * t;
 }
 
 }  // namespace lbk

@@ -71,6 +71,7 @@ LB_DS_BWD_FLOATS = 24704
 LB_DS_SETVEC_FLOATS = 904
 LB_DS_WGRAD_FLOATS = 4608
 LB_DS_WORKSPACE_FLOATS = 1024 * 2 * LB_DS_WGRAD_FLOATS
+LB_DS_OVER_SETS_SPAN = 256  # lb_ds_over_sets: sets per partial sum (workspace rows)
 LB_DS_SETGRAD_ACTOR, LB_DS_SETGRAD_CRITIC = 4736, 12800
 LB_DSV = {"MAX0": 0, "GA3": 8, "MAX2A": 72, "GS2A": 136, "MAX1A": 200, "GS1A": 264, "CS2": 328,
           "MAX2C": 392, "GS2C": 456, "MAX1C": 520, "GS1C": 584, "ID1A": 648, "ID2A": 680, "ID1C": 712,

@@ -93,14 +93,14 @@ def _over_sets(a, b, alpha=1.0):
     return out
 
 
-OS_SPAN = 1024  # lb_ds_over_sets' sets per partial sum
+OS_SPAN = _native.LB_DS_OVER_SETS_SPAN  # lb_ds_over_sets' sets per partial sum
 _os_work = {}
 
 
 def sums_over_sets(jobs, S, dev):
     """lb_ds_over_sets: for each job (a, b, scale) with a (S, M) or None (a plain sum of b's rows)
     and b (S, N) -- 2-D views with unit column stride -- the (M, N) tensor scale * a^T b, all jobs in
-    two launches (an MFMA partial sum per 1024-set span, then the spans added in order)."""
+    two launches (an MFMA partial sum per OS_SPAN-set span, then the spans added in order)."""
     outs, cjobs, row = [], [], 0
     for a, b, scale in jobs:
         M = 1 if a is None else a.shape[1]

@@ -474,10 +474,12 @@ int lb_ds_set_grads(const float* setvec, const float* dlogits, const float* dmea
 /* (ABI 12) Sums over a large batch of sets, the training step's remaining weight gradients at
  * PPO's minibatch size: for each job, out[m][n] = scale * sum_s A(s, m) B(s, n) with
  * A(s, m) = a[s lda + m] (a NULL: A(s, 0) = 1, M = 1, a plain sum of B's rows) and
- * B(s, n) = b[s ldb + n], 1 <= M, N <= 64, at most 16 jobs.  Two launches: each wave a 16 x 16
- * output tile over a span of 1024 sets on f32 MFMA into workspace, then the spans' partial sums
- * added in ascending order (deterministic).  workspace: ceil(num_sets / 1024) x sum(M N) floats.
- * Replaces per job a chunked GEMM and its reduction. */
+ * B(s, n) = b[s ldb + n], 1 <= M, N <= 64, at most 16 jobs (a or b 16-byte aligned with lda or
+ * ldb a multiple of 4: vector operand loads).  Two launches: each wave one job's whole output over a span
+ * of LB_DS_OVER_SETS_SPAN sets on f32 MFMA into workspace, then the spans' partial sums added in
+ * ascending order (deterministic).  workspace: ceil(num_sets / LB_DS_OVER_SETS_SPAN) x sum(M N)
+ * floats.  Replaces per job a chunked GEMM and its reduction. */
+#define LB_DS_OVER_SETS_SPAN 256
 typedef struct lb_set_job {
     const float* a;
     int64_t lda;

@@ -207,15 +207,17 @@ def test_ppo_head_matches_autograd(R, masked):
 def test_sums_over_sets_match_torch():
     """lb_ds_over_sets (the PPO minibatch's sums over 51,200 sets: Gamma / Lambda3 / rho weight
     gradients, bias sums) == float64 a^T b, for job shapes of the training step (M, N in {1, 8,
-    64}, a NULL = a plain sum), strided setvec-like views, and set counts that are not
-    multiples of the MFMA's 4 sets or the 1,024-set span; tolerance: f32 sums of S products."""
+    64}, a NULL = a plain sum; M = 20: a partly filled 4-tile job), strided setvec-like views
+    (aligned: float4 operand loads; offset by 10 floats: scalar loads), and set counts that are
+    not multiples of the MFMA's 4 sets or the 256-set span; tolerance: f32 sums of S products."""
     from lbk8s import fused_train
     g = torch.Generator(device="cuda").manual_seed(11)
     for S in (51200, 1500, 1023, 5):
         wide = torch.randn((S, 300), generator=g, device="cuda")
         jobs = [(wide[:, 0:64], wide[:, 100:108], -1.0), (wide[:, 64:128], wide[:, 128:192], 1.0),
                 (None, wide[:, 200:264], 1.0), (wide[:, 264:265], wide[:, 192:256], -1.0),
-                (wide[:, 10:74], wide[:, 290:291], 0.5), (None, wide[:, 299:300], 1.0)]
+                (wide[:, 10:74], wide[:, 290:291], 0.5), (None, wide[:, 299:300], 1.0),
+                (wide[:, 0:20], wide[:, 4:68], 2.0), (wide[:, 8:72], wide[:, 30:94], 1.0)]
         outs = fused_train.sums_over_sets(jobs, S, wide.device)
         for (a, b, sc), o in zip(jobs, outs):
             a64 = torch.ones((S, 1), dtype=torch.float64, device="cuda") if a is None else a.double()
