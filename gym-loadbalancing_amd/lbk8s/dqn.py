@@ -220,6 +220,10 @@ class DQN_DeepSets:
         self._dqn_sync = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._pgraphs = {}
         self._pgraph_slope = None
+        # consecutive train periods replayed as ONE graph (single rank): the host's per-period
+        # work (a graph launch, the replay-slot mirror, the train-step bookkeeping) otherwise
+        # left the GPU idle between periods (config 5: ~85 us per 10-step period)
+        self.periods_per_graph = max(1, int(os.environ.get("LBK8S_DQN_PERIODS_PER_GRAPH", "4")))
         self._tstatic = None
         # the target network's image, packed when the target changes (every
         # target_network_frequency steps), outside the captured periods
@@ -325,8 +329,12 @@ class DQN_DeepSets:
             self._sample_dev(parity ^ (n & 1))
             self._tloss = self._train_backward(*self._tstatic)
 
+    def _reps(self):
+        return 1 if self._multi else self.periods_per_graph
+
     def _build_period_graphs(self, obs, masks):
-        """Capture the period graphs: keys (n, train, parity) for n in {1, train_frequency}."""
+        """Capture the period graphs: keys (n, train, parity, reps) for n in {1, train_frequency};
+        reps > 1: that many consecutive train periods in one graph (single rank)."""
         F = self.train_frequency
         if self._tstatic is None:
             self._alloc_tstatic()
@@ -336,23 +344,44 @@ class DQN_DeepSets:
         # the same trajectory as an eager one
         self._train_warmup()
         graphs = {}
-        keys = sorted({(1, False), (F, False), (F, True)})
-        for n, train in keys:
+        keys = {(1, False, 1), (F, False, 1), (F, True, 1), (F, True, self._reps())}
+        for n, train, reps in sorted(keys):
             for parity in (0, 1):
                 self._tloss = None
                 ga = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(ga):
-                    self._period_body(obs, masks, n, train, parity)
-                    if train and not self._multi:
-                        self._train_apply()
+                    p = parity
+                    for _ in range(reps):
+                        self._period_body(obs, masks, n, train, p)
+                        if train and not self._multi:
+                            self._train_apply()
+                        p ^= n & 1
                 gs = (ga,)
                 if train and self._multi:
                     gb = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(gb):
                         self._train_apply()
                     gs = (ga, gb)
-                graphs[n, train, parity] = (gs, self._tloss)  # (each graph writes its own loss tensor)
+                # (each graph writes its own loss tensor: the last period's)
+                graphs[n, train, parity, reps] = (gs, self._tloss)
         return graphs
+
+    def _chunk(self, g, total_timesteps):
+        """How many consecutive train periods from step g (a period start) one graph replays:
+        periods_per_graph when each is a whole train period and none but the last ends on a
+        target-network update or holds a logged step, else 1."""
+        F, R = self.train_frequency, self._reps()
+        if R == 1:
+            return 1
+        for r in range(R):
+            g0 = g + r * F
+            last = g0 + F - 1
+            if not (g0 % F == 1 % F and g0 + F <= total_timesteps and last > self.learning_starts and last % F == 0):
+                return 1
+            if r < R - 1 and (last % self.target_network_frequency == 0
+                              or any(s % 1000 == 0 or s == total_timesteps - 1 for s in range(g0, last + 1))):
+                return 1
+        return R
 
     def _alloc_tstatic(self):
         B, rb = self.batch_size, self.rb
@@ -467,11 +496,12 @@ class DQN_DeepSets:
             last = g + n - 1
             train = last > self.learning_starts and last % F == 0
             if self.period_graph:
-                hit = self._pgraphs.get((n, train, self._parity))
+                reps = self._chunk(g, total_timesteps) if (n == F and train) else 1
+                hit = self._pgraphs.get((n, train, self._parity, reps))
                 if hit is None:  # (a step count the graphs do not hold)
-                    n, last = 1, g
+                    n, last, reps = 1, g, 1
                     train = last > self.learning_starts and last % F == 0
-                    hit = self._pgraphs[n, train, self._parity]
+                    hit = self._pgraphs[n, train, self._parity, reps]
                 gs, tloss = hit
                 gs[0].replay()
                 if len(gs) > 1:
@@ -479,6 +509,12 @@ class DQN_DeepSets:
                     gs[1].replay()
                 if train:
                     loss = tloss
+                for _ in range(reps - 1):  # (the chunk's earlier periods: the host mirror)
+                    for _ in range(n):
+                        self._parity ^= 1
+                        self.rb.advance_host()
+                    self._after_train(last)
+                    g, last = g + n, last + n
             else:
                 self._period_body(obs, masks, n, train, self._parity)
                 if train:

@@ -73,15 +73,20 @@ def test_dqn_multi_step_periods_match_single_steps():
     run as ONE lb_dqn_steps launch; the learner then follows exactly the trajectory of one
     lb_dqn_step launch per vector step: same replay contents, parameters, env state and
     episode sums (period graphs on both sides; 10-step periods, even, so the device words
-    are updated in place, and the 1-step periods around them)."""
+    are updated in place, and the 1-step periods around them).  Four train periods (steps
+    1-40, the last ending on the target sync) replay as one graph by default; one graph per
+    period (periods_per_graph = 1) follows the same trajectory."""
     from lbk8s import LBVecEnv
     from lbk8s.dqn import DQN_DeepSets
     res = []
-    for multi, prep in ((False, False), (True, False), (True, True)):
+    for multi, prep, ppg in ((False, False, 4), (True, False, 4), (True, True, 4), (True, False, 1)):
         env = LBVecEnv(4096, seed=4, as_tensors=True, episode_length=10)
-        algo = DQN_DeepSets(env, buffer_size=4096 * 40, batch_size=128, learning_starts=15, train_frequency=10,
+        algo = DQN_DeepSets(env, buffer_size=4096 * 40, batch_size=128, learning_starts=5, train_frequency=10,
                             target_network_frequency=40, seed=1, multi_step=multi)
+        algo.periods_per_graph = ppg
         assert algo.period_graph and env.dqn_steps_supported(env.cfg.obs_rows)
+        if ppg > 1:
+            assert algo._chunk(1, 62) == ppg and algo._chunk(41, 62) == 1
         if prep:  # (the graphs captured beforehand: nothing may move)
             algo.prepare(62)
         algo.learn(total_timesteps=62)
