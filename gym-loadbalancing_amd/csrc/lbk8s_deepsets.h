@@ -498,16 +498,18 @@ __device__ __forceinline__ void store_xrow(float* plane, float v, int64_t env, i
 }
 
 // one wave iteration's P envs: the observation -> layer-1 B fragments and its set-wise max
-// (XR: the extra row R - 1 = 16 TS into xr0, features 4kk + grp, and into the max)
+// (XR: the extra row R - 1 = 16 TS into xr0, features 4kk + grp, and into the max; xobs: the
+// group's observations elsewhere, env env0 + s at xobs + s R 8 -- lb_dqn_steps' LDS copy)
 template <int TS, int P, int MODE, bool XR = false>
 __device__ __forceinline__ void ds_group_obs(const DSParams& p, int64_t env0, int col, int grp, int R,
-                                             float (&h0)[P * TS][2], float (&m0)[2], float (&xr0)[2]) {
+                                             float (&h0)[P * TS][2], float (&m0)[2], float (&xr0)[2],
+                                             const float* xobs = nullptr) {
     constexpr bool TRAIN = MODE == 1;
     // obs -> layer-1 B fragments: k-step kk holds feature 4kk + grp of set element col
 #pragma unroll
     for (int s = 0; s < P; ++s) {
         const bool live = env0 + s < p.B;
-        const float* x = p.obs + (env0 + s) * (int64_t)R * 8;
+        const float* x = xobs ? xobs + s * R * 8 : p.obs + (env0 + s) * (int64_t)R * 8;
 #pragma unroll
         for (int t = 0; t < TS; ++t) {
             const int row = 16 * t + col;

@@ -48,6 +48,7 @@ struct DQNReplay {  // lb_replay_add's buffers
 // every block has read them: in and out may be the same words.  The counter wraps itself: the
 // last block's atomicInc (limit gridDim.x - 1) returns gridDim.x - 1 and stores 0, so a launch
 // that starts with *sync == 0 leaves it 0 with no separate store.
+constexpr int DQN_OBS_F4 = 34;  // float4s of an observation of R <= 17 rows (dqn_step_fusable: R <= 16)
 template <int P>
 __global__ __launch_bounds__(DS_BLOCK, 2) void k_dqn_step(DSParams d, Params e, DQNReplay r, int nsteps,
                                                          int32_t* sync) {
@@ -81,67 +82,80 @@ __global__ __launch_bounds__(DS_BLOCK, 2) void k_dqn_step(DSParams d, Params e, 
     const int R = d.R, col = lane & 15, grp = lane >> 4;
     const int64_t groups = (d.B + P - 1) / P, n4 = e.B * r.f4;
     const int s = lane >> 4, l16 = lane & 15;
+    // the group's observations across the launch's steps in LDS, two buffers (step i's input
+    // and its next observations): the Q forward and the replay rows read them there, so a step
+    // issues its stores and reads nothing back from global memory (round 6: each step waited
+    // for its obs stores to land, then re-read them -- two memory round trips per step)
+    __shared__ __attribute__((aligned(16))) float4 OB[NWB][2][P * DQN_OBS_F4];
+    const int f4 = r.f4;  // float4s per observation (2 R <= DQN_OBS_F4: host check)
+    float4(*ob)[P * DQN_OBS_F4] = OB[threadIdx.x >> 6];
     for (int64_t gi = wave; gi < groups; gi += nwaves) {
         const int64_t env0 = gi * P;
         // the env held in registers across the launch's steps (as k_rollout_slice): loaded and
         // observed once, its history counters and scalars stored after the last step
         const int64_t env = env0 + s;
         const bool live = s < P && env < e.B;
+        const int64_t j1 = (env0 + P < e.B ? env0 + P : e.B) * f4 - env0 * f4;  // the group's float4s
         SEnv<1> v;
         if (live) {
             slice_load<16, 1>(e, env, l16, v);
             slice_observe<1>(e, v);
         }
+        for (int j = lane; j < j1; j += 64) ob[0][j] = r.obs[env0 * f4 + j];
         for (int i = 0; i < nsteps; ++i) {
             const bool explore = (exm >> i) & 1u;
             const int64_t ps = (pos + i) % r.slots;
+            float4* cur = ob[i & 1];
+            float4* nxt = ob[(i + 1) & 1];
             // the greedy actions of the group's envs (lane s holds env0 + s's; :134-142)
             int32_t act = -1;
             if (!explore) {
                 float h0[P][2], m0[2];
                 float xr0[2];
-                ds_group_obs<1, P, 2>(d, env0, col, grp, R, h0, m0, xr0);
+                ds_group_obs<1, P, 2>(d, env0, col, grp, R, h0, m0, xr0, reinterpret_cast<const float*>(cur));
                 act = ds_group_actor<1, P, 2, true>(d, W, lane, env0, col, grp, R, h0, m0, xs);
             }
             const int32_t ag = __shfl(act, s < P ? s : 0);
             // the env step: lanes 16 s .. 16 s + 15 step env env0 + s (k_step_slice<16, 1>'s body,
             // the observed values kept in registers: a step changes the selected endpoint's)
             int a = 0;
+            float rw = 0.f;
+            bool dn = false;
+            double ret = 0.0;  // the finished episode's return (its ep_stats row's first column)
             if (live) {
                 a = explore ? random_action(e, env, v.acc3, v.s.step) : ag;  // (exploring: :128-131)
                 if (explore && l16 == 0) d.actions[env] = a;
                 const SPrep pr = slice_prep<16, 1>(e, v, a);
-                bool done;
-                const double reward = slice_apply<16, 1, false, false>(e, env, l16, v, pr, done);
+                const double tot0 = v.total;
+                const double reward = slice_apply<16, 1, false, false>(e, env, l16, v, pr, dn);
+                rw = (float)reward;
+                ret = e.auto_reset ? tot0 + reward : 0.0;  // (slice_apply's v.total += reward)
                 if (l16 == 0) {
-                    e.reward[env] = (float)reward;
+                    e.reward[env] = rw;
                     if (e.rew64) e.rew64[env] = reward;
-                    e.done[env] = (uint8_t)done;
+                    e.done[env] = (uint8_t)dn;
                 }
-                slice_obs<16, 1, P == 4 ? NWB : 0>(e, env, l16, v, e.obs);
+                slice_obs_rows<16, 1>(e, l16, v, [&](int q, float4 o) { nxt[s * f4 + q] = o; });
             }
-            // the group's replay rows (lb_replay_add's), once the step's outputs have landed
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const int64_t hi = (env0 + P < e.B ? env0 + P : e.B) * r.f4;
-            const float4* nxo = reinterpret_cast<const float4*>(e.obs);
-            for (int64_t j = env0 * r.f4 + lane; j < hi; j += 64) {
-                const float4 o = r.obs[j], nx = nxo[j];
-                r.rb_obs[ps * n4 + j] = o;
-                r.rb_next_obs[ps * n4 + j] = nx;
-                r.obs[j] = nx;
+            // the group's replay rows (lb_replay_add's) and obs <- next obs, from LDS (the
+            // wave's LDS writes and reads complete in order)
+            for (int j = lane; j < j1; j += 64) {
+                const float4 o = cur[j], nx = nxt[j];
+                const int64_t g = env0 * f4 + j;
+                r.rb_obs[ps * n4 + g] = o;
+                r.rb_next_obs[ps * n4 + g] = nx;
+                r.obs[g] = nx;
+                st_stream(reinterpret_cast<float4*>(e.obs) + g, nx);
             }
-            if (s < P && l16 == 0 && env < e.B) {  // (the lane that wrote the env's reward, done and stats row)
-                const bool dn = e.done[env] != 0;
+            if (live && l16 == 0) {  // (the lane that wrote the env's reward, done and stats row)
                 r.rb_actions[ps * e.B + env] = a;
-                r.rb_rewards[ps * e.B + env] = e.reward[env];
+                r.rb_rewards[ps * e.B + env] = rw;
                 r.rb_dones[ps * e.B + env] = dn ? 1.f : 0.f;
                 if (r.ep_sum && dn) {
-                    r.ep_sum[env] += e.ep_stats[env * LB_ST_K];
+                    r.ep_sum[env] += e.auto_reset ? ret : e.ep_stats[env * LB_ST_K];
                     r.ep_cnt[env] += 1.0;
                 }
             }
-            // (step i + 1 reads the obs and the sums back)
-            if (i + 1 < nsteps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         if (live) {
             if (l16 < e.E) e.edyn[eidx(e, env, l16)] = v.ed[0];

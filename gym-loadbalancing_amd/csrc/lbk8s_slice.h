@@ -93,10 +93,10 @@ struct SEnv {
 // row r = cW/2 + (l >> 1), h = l & 1.  Row r < E is endpoint r, held by lane r % W in
 // slot r / W = c >> 1, so each lane's halves come from lane (c & 1) W/2 + (l >> 1) by a
 // lane shuffle; the reject row (r = E) is the same on every lane.
-template <int W, int EPL>
-__device__ __forceinline__ void slice_write_obs(const Params& p, float* out, int64_t env, int lane,
-                                                const SEnv<EPL>& v) {
-    float4* base = reinterpret_cast<float4*>(out + env * (int64_t)p.R * 8);
+// (put(q, o): float4 q of the env's block; slice_write_obs streams it to out, lb_dqn_steps
+// keeps it in LDS)
+template <int W, int EPL, typename Put>
+__device__ __forceinline__ void slice_obs_rows(const Params& p, int lane, const SEnv<EPL>& v, Put&& put) {
     const float rz = (float)v.s.rz, thr = (float)threshold(v.s.thr_idx), dt = (float)v.dt;
     const int n4 = 2 * p.R, h = lane & 1;
 #pragma unroll
@@ -122,9 +122,15 @@ __device__ __forceinline__ void slice_write_obs(const Params& p, float* out, int
             // rows past E: the reject row (r == E, present iff R > E); later rows are past R
             const float4 o = (r < p.E && k < EPL) ? (h ? sb : sa)
                                                   : (h ? make_float4(-1.f, rz, thr, dt) : make_float4(-1.f, -1.f, -1.f, -1.f));
-            if (q < n4) st_stream(base + q, o);
+            if (q < n4) put(q, o);
         }
     }
+}
+template <int W, int EPL>
+__device__ __forceinline__ void slice_write_obs(const Params& p, float* out, int64_t env, int lane,
+                                                const SEnv<EPL>& v) {
+    float4* base = reinterpret_cast<float4*>(out + env * (int64_t)p.R * 8);
+    slice_obs_rows<W, EPL>(p, lane, v, [&](int q, float4 o) { st_stream(base + q, o); });
 }
 
 // get_state() for the 4 envs of a wave (W = 16) as ONE contiguous run: the envs' R x 32-byte
