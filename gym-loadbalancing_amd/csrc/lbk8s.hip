@@ -1226,17 +1226,13 @@ int lb_ds_train_backward(const float* bwd_frag, const float* obs, int64_t num_en
                   num_envs, num_elements, actor, critic};
     // fixed grid: one workspace slot per block, so the reduction order never depends on B
     hipStream_t s = (hipStream_t)stream;
-    // each head: the backward, then layer 1's pooled term added to its slots
+    // each head's backward (layer 1's pooled term in its slots too)
     if (actor) {
         hipLaunchKernelGGL(k_ds_train_bwd<0>, dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);
-        if (int r = check_launch()) return r;
-        hipLaunchKernelGGL(k_ds_l1_pool<0>, dim3(DSW_GRID), dim3(64 * DSL_SUB), 0, s, p);
         if (int r = check_launch()) return r;
     }
     if (critic) {
         hipLaunchKernelGGL(k_ds_train_bwd<1>, dim3(DSW_GRID), dim3(DSB_BLOCK), 0, s, p);
-        if (int r = check_launch()) return r;
-        hipLaunchKernelGGL(k_ds_l1_pool<1>, dim3(DSW_GRID), dim3(64 * DSL_SUB), 0, s, p);
         if (int r = check_launch()) return r;
     }
     static_assert(DSW_SLOTS % (2 * DSR_GROUPS) == 0, "reduction stride");

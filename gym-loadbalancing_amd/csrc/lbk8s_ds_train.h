@@ -54,7 +54,7 @@ enum : int {
     DSV_ID2A = 680,
     DSV_ID1C = 712,
     DSV_ID2C = 744,
-    DSV_P1A = 776,    // actor: layer 1's pooled term per feature, V act'(MAX1) (k_ds_l1_pool)
+    DSV_P1A = 776,    // actor: layer 1's pooled term per feature, V act'(MAX1)
     DSV_P1C = 840,    // critic
     DSV_FLOATS = 904,
 };
@@ -108,7 +108,7 @@ __device__ __forceinline__ float dact(float y) {
 //     terms and of dz1;
 //   per set, after its last tile: sum_r dz2 in closed form, V = Gamma2^T sum_r dz2, layer
 //     1's pooled term (dz1 at row ID1[o] of feature o carries -V[o] act'(MAX1[o]): one row
-//     per feature, folded into sum_r dz1 here and into dLambda1 by k_ds_l1_pool), the set
+//     per feature, folded into sum_r dz1 and, with the obs row at ID1[o], into dLambda1), the set
 //     sums out.
 // Each set's small inputs (dlogits or dmean, ID2, MAX2) are loaded one set ahead.
 //
@@ -138,6 +138,7 @@ struct SetIn {
     uint2 id2;       // ID2 rows (u16) of features 4col .. 4col + 3
     float4 mx2;      // MAX2 of features 4col .. 4col + 3
     float mx1;       // MAX1 of feature lane
+    uint32_t id1;    // ID1 row of feature lane (layer 1's pooled term, below)
 };
 
 template <int HEAD>
@@ -173,6 +174,7 @@ __device__ __forceinline__ void load_setin(const DSBwdParams& p, int64_t env, in
                                             4 * col);
     s.mx2 = *reinterpret_cast<const float4*>(sv + (HEAD == 0 ? DSV_MAX2A : DSV_MAX2C) + 4 * col);
     s.mx1 = sv[(HEAD == 0 ? DSV_MAX1A : DSV_MAX1C) + lane];
+    s.id1 = reinterpret_cast<const uint16_t*>(sv + (HEAD == 0 ? DSV_ID1A : DSV_ID1C))[lane];
 }
 
 // lane-per-feature matrix-vector product out[lane] = sum_i M[i][lane] x[i], M natural
@@ -203,6 +205,8 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
     __shared__ __attribute__((aligned(16))) float TB[DSB_WAVES][DST_FLOATS];
     // per wave: [0, 64) broadcast scratch, c1 [64, 128), c2 [128, 192) of the current set
     __shared__ __attribute__((aligned(16))) float CV[DSB_WAVES][DSB_CV];
+    // per wave: layer 1's pooled term in dLambda1, lane o's row (8 floats), summed over its sets
+    __shared__ __attribute__((aligned(16))) float POOL[DSB_WAVES][64 * 8];
     {
         // fragment image -> natural order: fragment (nt, k), lane l holds W^T[o][i] with
         // o = 16nt + (l & 15), i = 16(k >> 2) + 4(l >> 4) + (k & 3)
@@ -227,6 +231,9 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
     const int64_t nwaves = (int64_t)gridDim.x * DSB_WAVES;
     float* la = TB[wv];
     float* cv = CV[wv];
+    float4* pool = reinterpret_cast<float4*>(POOL[wv]) + 2 * lane;
+    pool[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+    pool[1] = make_float4(0.f, 0.f, 0.f, 0.f);
     const int R = p.R, ntl = (R + 15) / 16;
     const int nct = ((R - 1) % 16) / 4 + 1;  // 4-row groups of the last tile that hold set rows
     const bool one_row = R % 16 == 1;        // the last tile holds one set row (below)
@@ -247,6 +254,7 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
         auto env_of = [&](int64_t j) { return env0 + j * nwaves; };
         // per-set state (W layout: this lane's rows, features 4col .. 4col + 3)
         float S4[4], G4[4], gs1[4], g3 = 0.f;
+        float4 xid0, xid1;  // the obs row at ID1 of this lane's feature
         uint2 id2w = make_uint2(0u, 0u);
         float4 mx2v;
         float mx1l = 0.f;
@@ -262,6 +270,13 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
             id2w = cur.id2;
             mx2v = cur.mx2;
             mx1l = cur.mx1;
+            // the obs row at ID1 of this lane's feature (used by the epilogue: in flight
+            // across the set's tiles)
+            {
+                const float4* xr = reinterpret_cast<const float4*>(p.obs + (env_of(j) * (int64_t)R + cur.id1) * 8);
+                xid0 = xr[0];
+                xid1 = xr[1];
+            }
             float c1, c2;
             if (HEAD == 0) {
                 float s = cur.dls;
@@ -320,7 +335,22 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
             if (grp == 0)
                 *reinterpret_cast<float4*>(sv + (HEAD == 0 ? DSV_GS1A : DSV_GS1C) + 4 * col) =
                     make_float4(gs1[0], gs1[1], gs1[2], gs1[3]);
-            sv[(HEAD == 0 ? DSV_P1A : DSV_P1C) + lane] = corr;  // -> k_ds_l1_pool (dLambda1)
+            sv[(HEAD == 0 ? DSV_P1A : DSV_P1C) + lane] = corr;
+            // ... and in dLambda1: dLambda1[o][c] -= corr[o] obs[ID1[o]][c] (lane o; subtracted
+            // from the block's slot after the waves' sums)
+            {
+                float4 q0 = pool[0], q1 = pool[1];
+                q0.x += corr * xid0.x;
+                q0.y += corr * xid0.y;
+                q0.z += corr * xid0.z;
+                q0.w += corr * xid0.w;
+                q1.x += corr * xid1.x;
+                q1.y += corr * xid1.y;
+                q1.z += corr * xid1.z;
+                q1.w += corr * xid1.w;
+                pool[0] = q0;
+                pool[1] = q1;
+            }
 #pragma unroll
             for (int m = 0; m < 4; ++m) S4[m] = G4[m] = gs1[m] = 0.f;
         };
@@ -517,57 +547,16 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
                         r = w == 0 ? w1[mt][i] : r + w1[mt][i];
                     }
                 }
+            // (the wave's own LDS accesses complete in order)
+            const float4 q0 = pool[0], q1 = pool[1];
+            const float pq[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+            for (int c = 0; c < 8; ++c) red[4096 + lane * 8 + c] -= pq[c];
         }
         __syncthreads();
     }
     float* slot = p.wpart + (int64_t)blockIdx.x * (2 * DSW_FLOATS) + HEAD * DSW_FLOATS;
     for (int i = threadIdx.x; i < DSW_FLOATS; i += DSB_BLOCK) slot[i] = red[i];
-}
-
-// Layer 1's pooled term in dLambda1: dz1 at row ID1[o] of feature o carries -P1[o] (the
-// backward's per-set P1 = V act'(MAX1)), so dLambda1[o][c] -= sum_sets P1[o] obs[ID1[o]][c].
-// Block b adds its share to workspace slot b of the head (after k_ds_train_bwd wrote it):
-// thread (o, sub) walks sets sub, sub + DSL_SUB, ... of the block's, two sets per iteration
-// (independent gathers in flight), 8 accumulators; the subgroups are summed in LDS in a
-// fixed order.
-constexpr int DSL_SUB = 16;  // set subgroups per block (1,024 threads)
-template <int HEAD>
-__global__ __launch_bounds__(64 * DSL_SUB) void k_ds_l1_pool(DSBwdParams p) {
-    __shared__ float part[DSL_SUB][512];
-    const int o = threadIdx.x & 63, sub = threadIdx.x >> 6;
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    const int64_t stride = (int64_t)gridDim.x * DSL_SUB;
-    auto term = [&](int64_t s) {
-        const float* sv = p.setvec + s * (int64_t)DSV_FLOATS;
-        const float c = sv[(HEAD == 0 ? DSV_P1A : DSV_P1C) + o];
-        const int r = reinterpret_cast<const uint16_t*>(sv + (HEAD == 0 ? DSV_ID1A : DSV_ID1C))[o];
-        const float4* x = reinterpret_cast<const float4*>(p.obs + (s * (int64_t)p.R + r) * 8);
-        const float4 x0 = x[0], x1 = x[1];
-        acc[0] += c * x0.x;
-        acc[1] += c * x0.y;
-        acc[2] += c * x0.z;
-        acc[3] += c * x0.w;
-        acc[4] += c * x1.x;
-        acc[5] += c * x1.y;
-        acc[6] += c * x1.z;
-        acc[7] += c * x1.w;
-    };
-    int64_t s = (int64_t)blockIdx.x * DSL_SUB + sub;
-    for (; s + stride < p.B; s += 2 * stride) {
-        term(s);
-        term(s + stride);
-    }
-    if (s < p.B) term(s);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) part[sub][o * 8 + k] = acc[k];
-    __syncthreads();
-    float* slot = p.wpart + (int64_t)blockIdx.x * (2 * DSW_FLOATS) + HEAD * DSW_FLOATS + 4096;
-    if (threadIdx.x < 512) {
-        float t = 0.f;
-#pragma unroll
-        for (int g = 0; g < DSL_SUB; ++g) t += part[g][threadIdx.x];
-        slot[threadIdx.x] -= t;
-    }
 }
 
 // sum of the per-wave partials: out[j] = sum_s wpart[s][j], j < 2 * DSW_FLOATS; zeros for
