@@ -1210,9 +1210,39 @@ int lb_ds_pack_pair(const lb_ds_weights* w, float* frag_out, float* bwd_frag_out
     return check_launch();
 }
 
-int lb_ds_train_backward(const float* bwd_frag, const float* obs, int64_t num_envs, int32_t num_elements,
-                         const float* save_actor, const float* save_critic, const float* dlogits, const float* dmean,
-                         float* wgrad_out, float* workspace, float* setvec, void* stream) {
+}  // extern "C"
+namespace {
+// lb_ds_set_grads' jobs (returns their count)
+int set_grad_params(const float* setvec, const float* dlogits, const float* dmean, int64_t num_sets,
+                    int32_t num_elements, float* out, SetGradParams& p) {
+    const int SV = LB_DS_SETVEC_FLOATS;
+    p = SetGradParams{};
+    p.S = num_sets;
+    int nj = 0;
+    auto job = [&](const float* a, int lda, int M, int amode, int alen, int boff, const float* b, int ldb, int N,
+                   float scale, float* o) {
+        p.job[nj++] = SetGradJob{a, lda, M, amode, alen, b ? b : setvec + boff, ldb, N, scale, o};
+    };
+    // actor: dGamma1 = -GS1A^T MAX0, dGamma2 = -GS2A^T MAX1A, dLambda3 = sum GA3,
+    // dGamma3 = -(row sums of dlogits)^T MAX2A
+    job(setvec + LB_DSV_GS1A, SV, 64, 0, 0, LB_DSV_MAX0, nullptr, SV, 8, -1.f, out);
+    job(setvec + LB_DSV_GS2A, SV, 64, 0, 0, LB_DSV_MAX1A, nullptr, SV, 64, -1.f, out + 512);
+    job(nullptr, 0, 1, 1, 0, LB_DSV_GA3, nullptr, SV, 64, 1.f, out + 4608);
+    job(dlogits, num_elements, 1, 2, num_elements, LB_DSV_MAX2A, nullptr, SV, 64, -1.f, out + 4672);
+    if (dmean) {  // critic: the same for psi, layer 3 from dmean (the mean's 1/R on Lambda3)
+        float* c = out + LB_DS_SETGRAD_ACTOR;
+        job(setvec + LB_DSV_GS1C, SV, 64, 0, 0, LB_DSV_MAX0, nullptr, SV, 8, -1.f, c);
+        job(setvec + LB_DSV_GS2C, SV, 64, 0, 0, LB_DSV_MAX1C, nullptr, SV, 64, -1.f, c + 512);
+        job(dmean, 64, 64, 0, 0, LB_DSV_CS2, nullptr, SV, 64, 1.f / (float)num_elements, c + 4608);
+        job(dmean, 64, 64, 0, 0, LB_DSV_MAX2C, nullptr, SV, 64, -1.f, c + 8704);
+    }
+    static_assert(LB_DS_SETGRAD_ACTOR == 4736 && LB_DS_SETGRAD_CRITIC == 12800, "set-gradient layout");
+    return nj;
+}
+// the training backward's launches (set_grads_out: lb_ds_train_backward_sets)
+int train_backward(const float* bwd_frag, const float* obs, int64_t num_envs, int32_t num_elements,
+                   const float* save_actor, const float* save_critic, const float* dlogits, const float* dmean,
+                   float* wgrad_out, float* workspace, float* setvec, float* set_grads_out, void* stream) {
     static_assert(DSV_FLOATS == LB_DS_SETVEC_FLOATS, "per-set vector layout and header disagree");
     static_assert(DSW_FLOATS == LB_DS_WGRAD_FLOATS && DSW_SLOTS * 2 * DSW_FLOATS <= LB_DS_WORKSPACE_FLOATS,
                   "weight-gradient layout and header disagree");
@@ -1236,9 +1266,34 @@ int lb_ds_train_backward(const float* bwd_frag, const float* obs, int64_t num_en
         if (int r = check_launch()) return r;
     }
     static_assert(DSW_SLOTS % (2 * DSR_GROUPS) == 0, "reduction stride");
-    hipLaunchKernelGGL(k_ds_wgrad_reduce, dim3((2 * DSW_FLOATS + DSR_COLS - 1) / DSR_COLS), dim3(DSR_COLS * DSR_GROUPS),
-                       0, s, workspace, wgrad_out, (int)actor, (int)critic);
+    if (set_grads_out) {
+        SetGradParams sg;
+        const int nj = set_grad_params(setvec, dlogits, dmean, num_envs, num_elements, set_grads_out, sg);
+        hipLaunchKernelGGL(k_ds_wgrad_reduce_sets, dim3(DSR_BLOCKS + SG_TILES * nj), dim3(SG_THREADS), 0, s, workspace,
+                           wgrad_out, (int)actor, (int)critic, sg);
+        return check_launch();
+    }
+    hipLaunchKernelGGL(k_ds_wgrad_reduce, dim3(DSR_BLOCKS), dim3(DSR_COLS * DSR_GROUPS), 0, s, workspace, wgrad_out,
+                       (int)actor, (int)critic);
     return check_launch();
+}
+}  // namespace
+extern "C" {
+
+int lb_ds_train_backward(const float* bwd_frag, const float* obs, int64_t num_envs, int32_t num_elements,
+                         const float* save_actor, const float* save_critic, const float* dlogits, const float* dmean,
+                         float* wgrad_out, float* workspace, float* setvec, void* stream) {
+    return train_backward(bwd_frag, obs, num_envs, num_elements, save_actor, save_critic, dlogits, dmean, wgrad_out,
+                          workspace, setvec, nullptr, stream);
+}
+
+int lb_ds_train_backward_sets(const float* bwd_frag, const float* obs, int64_t num_envs, int32_t num_elements,
+                              const float* save_actor, const float* save_critic, const float* dlogits,
+                              const float* dmean, float* wgrad_out, float* workspace, float* setvec,
+                              float* set_grads_out, void* stream) {
+    if (!set_grads_out || !dlogits) return fail("lb_ds_train_backward_sets: set_grads_out and dlogits are required");
+    return train_backward(bwd_frag, obs, num_envs, num_elements, save_actor, save_critic, dlogits, dmean, wgrad_out,
+                          workspace, setvec, set_grads_out, stream);
 }
 
 int lb_ds_over_sets(const lb_set_job* jobs, int32_t num_jobs, int64_t num_sets, float* workspace,
@@ -1276,30 +1331,9 @@ int lb_ds_set_grads(const float* setvec, const float* dlogits, const float* dmea
     if (!setvec || !dlogits || !out || num_sets < 1) return fail("setvec/dlogits/out NULL or num_sets < 1");
     if (num_elements < 1 || num_elements > LB_DS_MAX_ELEMENTS_TRAIN)
         return fail("num_elements must be in [1, 257] (LB_DS_MAX_ELEMENTS_TRAIN)");
-    const int SV = LB_DS_SETVEC_FLOATS;
-    SetGradParams p{};
-    p.S = num_sets;
-    int nj = 0;
-    auto job = [&](const float* a, int lda, int M, int amode, int alen, int boff, const float* b, int ldb, int N,
-                   float scale, float* o) {
-        p.job[nj++] = SetGradJob{a, lda, M, amode, alen, b ? b : setvec + boff, ldb, N, scale, o};
-    };
-    // actor: dGamma1 = -GS1A^T MAX0, dGamma2 = -GS2A^T MAX1A, dLambda3 = sum GA3,
-    // dGamma3 = -(row sums of dlogits)^T MAX2A
-    job(setvec + LB_DSV_GS1A, SV, 64, 0, 0, LB_DSV_MAX0, nullptr, SV, 8, -1.f, out);
-    job(setvec + LB_DSV_GS2A, SV, 64, 0, 0, LB_DSV_MAX1A, nullptr, SV, 64, -1.f, out + 512);
-    job(nullptr, 0, 1, 1, 0, LB_DSV_GA3, nullptr, SV, 64, 1.f, out + 4608);
-    job(dlogits, num_elements, 1, 2, num_elements, LB_DSV_MAX2A, nullptr, SV, 64, -1.f, out + 4672);
-    if (dmean) {  // critic: the same for psi, layer 3 from dmean (the mean's 1/R on Lambda3)
-        float* c = out + LB_DS_SETGRAD_ACTOR;
-        job(setvec + LB_DSV_GS1C, SV, 64, 0, 0, LB_DSV_MAX0, nullptr, SV, 8, -1.f, c);
-        job(setvec + LB_DSV_GS2C, SV, 64, 0, 0, LB_DSV_MAX1C, nullptr, SV, 64, -1.f, c + 512);
-        job(dmean, 64, 64, 0, 0, LB_DSV_CS2, nullptr, SV, 64, 1.f / (float)num_elements, c + 4608);
-        job(dmean, 64, 64, 0, 0, LB_DSV_MAX2C, nullptr, SV, 64, -1.f, c + 8704);
-    }
-    static_assert(LB_DS_SETGRAD_ACTOR == 4736 && LB_DS_SETGRAD_CRITIC == 12800, "set-gradient layout");
-    hipLaunchKernelGGL(k_ds_set_grads, dim3((64 * 64 + SG_THREADS - 1) / SG_THREADS, nj), dim3(SG_THREADS), 0,
-                       (hipStream_t)stream, p);
+    SetGradParams p;
+    const int nj = set_grad_params(setvec, dlogits, dmean, num_sets, num_elements, out, p);
+    hipLaunchKernelGGL(k_ds_set_grads, dim3(SG_TILES, nj), dim3(SG_THREADS), 0, (hipStream_t)stream, p);
     return check_launch();
 }
 

@@ -564,11 +564,11 @@ __global__ __launch_bounds__(DSB_BLOCK, 1) void k_ds_train_bwd(DSBwdParams p) {
 // slot), combined through LDS in a fixed order: deterministic, and 1,152 blocks x 128
 // loads per thread instead of one 1,024-long chain per output.
 constexpr int DSR_COLS = 64, DSR_GROUPS = 8;
-__global__ __launch_bounds__(DSR_COLS * DSR_GROUPS) void k_ds_wgrad_reduce(const float* wpart, float* out, int actor,
-                                                                           int critic) {
-    __shared__ float part[DSR_GROUPS][DSR_COLS];
+constexpr int DSR_BLOCKS = (2 * DSW_FLOATS + DSR_COLS - 1) / DSR_COLS;
+__device__ __forceinline__ void ds_wgrad_reduce_body(const float* wpart, float* out, int actor, int critic, int blk,
+                                                     float (*part)[DSR_COLS]) {
     const int c = threadIdx.x % DSR_COLS, g = threadIdx.x / DSR_COLS;
-    const int j = blockIdx.x * DSR_COLS + c;
+    const int j = blk * DSR_COLS + c;
     const bool live = j < 2 * DSW_FLOATS && (j < DSW_FLOATS ? actor : critic);
     float s0 = 0.f, s1 = 0.f;
     if (live)
@@ -584,6 +584,11 @@ __global__ __launch_bounds__(DSR_COLS * DSR_GROUPS) void k_ds_wgrad_reduce(const
         for (int k = 0; k < DSR_GROUPS; ++k) t += part[k][c];
         out[j] = live ? t : 0.f;
     }
+}
+__global__ __launch_bounds__(DSR_COLS * DSR_GROUPS) void k_ds_wgrad_reduce(const float* wpart, float* out, int actor,
+                                                                           int critic) {
+    __shared__ float part[DSR_GROUPS][DSR_COLS];
+    ds_wgrad_reduce_body(wpart, out, actor, critic, blockIdx.x, part);
 }
 
 // PPO loss head (envs/ppo_deepset.py:227-263 on a minibatch): per set, from the logits
@@ -816,7 +821,8 @@ struct SetGradJob {
     float scale;
     float* out;      // [M][N]
 };
-constexpr int SG_JOBS = 8, SG_CH = 64, SG_THREADS = 256, SG_PER = SG_CH * 64 / SG_THREADS;
+constexpr int SG_JOBS = 8, SG_CH = 64, SG_THREADS = 512, SG_PER = SG_CH * 64 / SG_THREADS;
+constexpr int SG_TILES = 64 * 64 / SG_THREADS;  // blocks per job
 struct SetGradParams {
     SetGradJob job[SG_JOBS];
     int64_t S;
@@ -824,10 +830,11 @@ struct SetGradParams {
 
 // a chunk's loads are all issued before the first is used (the DQN's 128 sets: two chunks,
 // two memory round trips per block); the row sums take 4 lanes per set
-__global__ __launch_bounds__(SG_THREADS) void k_ds_set_grads(SetGradParams p) {
-    __shared__ float sa[SG_CH][64], sb[SG_CH][64];
-    const SetGradJob j = p.job[blockIdx.y];
-    const int tile = blockIdx.x * SG_THREADS;
+// (block (bx, by): job by, outputs bx SG_THREADS ..; sa, sb: the block's LDS chunk buffers)
+__device__ __forceinline__ void ds_set_grads_body(const SetGradParams& p, int bx, int by, float (*sa)[64],
+                                                  float (*sb)[64]) {
+    const SetGradJob j = p.job[by];
+    const int tile = bx * SG_THREADS;
     if (tile >= j.M * j.N) return;  // (block-uniform)
     const int e = tile + threadIdx.x;
     const bool on = e < j.M * j.N;
@@ -872,6 +879,25 @@ __global__ __launch_bounds__(SG_THREADS) void k_ds_set_grads(SetGradParams p) {
             for (int s = 0; s < cs; ++s) acc += sa[s][m] * sb[s][n];
     }
     if (on) j.out[e] = j.scale * acc;
+}
+__global__ __launch_bounds__(SG_THREADS) void k_ds_set_grads(SetGradParams p) {
+    __shared__ float sa[SG_CH][64], sb[SG_CH][64];
+    ds_set_grads_body(p, blockIdx.x, blockIdx.y, sa, sb);
+}
+// lb_ds_train_backward_sets: the weight-gradient slot reduction and the set-gradient jobs in one
+// launch (blocks below DSR_BLOCKS reduce, the rest are k_ds_set_grads' blocks): the DQN train
+// step's two last launches after the backward
+static_assert(SG_THREADS == DSR_COLS * DSR_GROUPS, "one block size for both parts");
+__global__ __launch_bounds__(SG_THREADS) void k_ds_wgrad_reduce_sets(const float* wpart, float* out, int actor,
+                                                                    int critic, SetGradParams sg) {
+    __shared__ float part[DSR_GROUPS][DSR_COLS];
+    __shared__ float sa[SG_CH][64], sb[SG_CH][64];
+    if ((int)blockIdx.x < DSR_BLOCKS) {
+        ds_wgrad_reduce_body(wpart, out, actor, critic, blockIdx.x, part);
+    } else {
+        const int v = blockIdx.x - DSR_BLOCKS;
+        ds_set_grads_body(sg, v % SG_TILES, v / SG_TILES, sa, sb);
+    }
 }
 
 // ---- lb_ds_over_sets: out[m][n] = scale * sum_s A(s, m) B(s, n) over a large batch of sets

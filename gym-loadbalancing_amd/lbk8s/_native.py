@@ -16,7 +16,7 @@ CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
 SOURCES = ("lbk8s.hip", "lbk8s_common.h", "lbk8s_slice.h", "lbk8s_tpe.h", "lbk8s_rollout.h", "lbk8s_lean.h",
            "lbk8s_deepsets.h", "lbk8s_ds_train.h", "lbk8s_dqn.h", "../../include/lbk8s.h", "lbk8s_lean_launch.h",
            "lbk8s_lean_inst.hip", "lbk8s_build.cpp")
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 LB_REWARD = {"naive": 0, "latency": 1, "fairness": 2, "multi": 3}
 LB_RNG_PHILOX, LB_RNG_TRACE = 0, 1
@@ -224,6 +224,7 @@ def lib():
     L.lb_dqn_head.argtypes = [vp, vp, vp, vp, vp, i64, i32, C.c_float, vp, vp, vp, vp, vp, vp]
     L.lb_replay_sample.argtypes = [i64, i32, i64, i32, C.c_uint64] + [vp] * 12 + [vp]
     L.lb_ds_set_grads.argtypes = [vp, vp, vp, i64, i32, vp, vp]
+    L.lb_ds_train_backward_sets.argtypes = [vp, vp, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.lb_ds_over_sets.argtypes = [C.POINTER(LBSetJobC), i32, i64, vp, i64, vp]
     for f in ("lb_validate_config", "lb_state_bytes", "lb_init", "lb_reset", "lb_step", "lb_policy", "lb_rollout",
               "lb_rollout_kernel", "lb_reward64",
@@ -231,7 +232,8 @@ def lib():
               "lb_ds_train_forward", "lb_ds_pack_backward", "lb_ds_train_backward", "lb_ds_q_argmax",
               "lb_replay_add", "lb_ppo_head", "lb_episode_log", "lb_dqn_act", "lb_dqn_head",
               "lb_replay_sample", "lb_ds_set_grads", "lb_dqn_step", "lb_dqn_steps",
-              "lb_dqn_steps_supported", "lb_ds_pack_pair", "lb_ds_forward_pair", "lb_ds_over_sets"):
+              "lb_dqn_steps_supported", "lb_ds_pack_pair", "lb_ds_forward_pair", "lb_ds_over_sets",
+              "lb_ds_train_backward_sets"):
         getattr(L, f).restype = C.c_int
     v = L.lb_abi_version()
     if v != ABI_VERSION and product:
@@ -269,4 +271,4 @@ EXPORTED_SYMBOLS = ("lb_abi_version", "lb_last_error", "lb_validate_config", "lb
                     "lb_rollout_kernel", "lb_source_hash", "lb_build_flags", "lb_build_compiler", "lb_reward64",
                     "lb_dqn_step",
                     "lb_dqn_steps", "lb_dqn_steps_supported", "lb_ds_pack_pair", "lb_ds_forward_pair",
-                    "lb_ds_over_sets")
+                    "lb_ds_over_sets", "lb_ds_train_backward_sets")

@@ -164,14 +164,13 @@ class _FusedDeepSetsTrain(torch.autograd.Function):
             bfrag = _pack_backward(actor_net, critic, dev)
         wgrad = torch.empty((2, _native.LB_DS_WGRAD_FLOATS), dtype=torch.float32, device=dev)
         work = _workspace(dev)
-        _native.check(_native.lib().lb_ds_train_backward(
-            bfrag.data_ptr(), x.data_ptr(), B, R, save_a.data_ptr(), fused._ptr(save_c), dlogits.data_ptr(),
-            fused._ptr(dmean), wgrad.data_ptr(), work.data_ptr(), setvec.data_ptr(), _stream(dev)))
-        if B <= SET_GRADS_MAX_SETS:  # the sums over the sets in one launch (lb_ds_set_grads)
+        args = (bfrag.data_ptr(), x.data_ptr(), B, R, save_a.data_ptr(), fused._ptr(save_c), dlogits.data_ptr(),
+                fused._ptr(dmean), wgrad.data_ptr(), work.data_ptr(), setvec.data_ptr())
+        if B <= SET_GRADS_MAX_SETS:
+            # the sums over the sets with the slot reduction, in its launch (lb_ds_train_backward_sets)
             n = _native.LB_DS_SETGRAD_ACTOR + (_native.LB_DS_SETGRAD_CRITIC if critic is not None else 0)
             sg = torch.empty(n, dtype=torch.float32, device=dev)
-            _native.check(_native.lib().lb_ds_set_grads(setvec.data_ptr(), dlogits.data_ptr(), fused._ptr(dmean),
-                                                        B, R, sg.data_ptr(), _stream(dev)))
+            _native.check(_native.lib().lb_ds_train_backward_sets(*args, sg.data_ptr(), _stream(dev)))
             grads = [wgrad[0, 4096:].view(64, 8), sg[:512].view(64, 8), wgrad[0, :4096].view(64, 64),
                      sg[512:4608].view(64, 64), sg[4608:4672].view(1, 64), sg[4672:4736].view(1, 64)]
             if critic is not None:
@@ -179,6 +178,7 @@ class _FusedDeepSetsTrain(torch.autograd.Function):
                 grads += [wgrad[1, 4096:].view(64, 8), c[:512].view(64, 8), wgrad[1, :4096].view(64, 64),
                           c[512:4608].view(64, 64), c[4608:8704].view(64, 64), c[8704:].view(64, 64)]
             return (None, None, None, None) + tuple(grads)
+        _native.check(_native.lib().lb_ds_train_backward(*args, _stream(dev)))
         # the sums over the sets, every one in one lb_ds_over_sets call (two launches)
         max0 = _vec(setvec, "MAX0", 8)
         g3 = dlogits.sum(1, keepdim=True)

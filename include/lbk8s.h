@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define LBK8S_ABI_VERSION 13
+#define LBK8S_ABI_VERSION 14
 
 /* reward_function names of loadbalancer_k8s_env.py:20-31 */
 enum { LB_REWARD_NAIVE = 0, LB_REWARD_LATENCY = 1, LB_REWARD_FAIRNESS = 2, LB_REWARD_MULTI = 3 };
@@ -470,6 +470,15 @@ int lb_ds_train_backward(const float* bwd_frag, const float* obs, int64_t num_en
 #define LB_DS_SETGRAD_CRITIC 12800
 int lb_ds_set_grads(const float* setvec, const float* dlogits, const float* dmean, int64_t num_sets,
                     int32_t num_elements, float* out, void* stream);
+
+/* (ABI 14) lb_ds_train_backward followed by lb_ds_set_grads (dlogits required; set_grads_out
+ * as lb_ds_set_grads' out), the weight-gradient slot reduction and the set-gradient jobs in one
+ * launch: the small-batch train step (the DQN's 128 sets) one launch shorter.  Same results as
+ * the two calls. */
+int lb_ds_train_backward_sets(const float* bwd_frag, const float* obs, int64_t num_envs, int32_t num_elements,
+                              const float* save_actor, const float* save_critic, const float* dlogits,
+                              const float* dmean, float* wgrad_out, float* workspace, float* setvec,
+                              float* set_grads_out, void* stream);
 
 /* (ABI 12) Sums over a large batch of sets, the training step's remaining weight gradients at
  * PPO's minibatch size: for each job, out[m][n] = scale * sum_s A(s, m) B(s, n) with

@@ -224,3 +224,44 @@ def test_sums_over_sets_match_torch():
             ref = sc * a64.t() @ b.double()
             assert o.shape == ref.shape
             torch.testing.assert_close(o.double(), ref, rtol=1e-4, atol=1e-4 * (S ** 0.5))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("critic", [True, False])
+def test_train_backward_sets_equals_two_calls(critic):
+    """lb_ds_train_backward_sets (the slot reduction and the set-gradient jobs in one launch,
+    the DQN train step's path) == lb_ds_train_backward then lb_ds_set_grads, bit for bit."""
+    from lbk8s import _native, fused, fused_train
+    agent = _agent(11).cuda()
+    B, R = 128, 9
+    dev = torch.device("cuda")
+    x = _inputs(B, R, seed=5).cuda()
+    crit = agent.critic if critic else None
+    frag = fused.packed(agent, agent.actor.net, crit)
+    logits = torch.empty((B, R), device=dev)
+    save_a = torch.empty((2, B, R, 64), device=dev)
+    setvec = torch.empty((B, _native.LB_DS_SETVEC_FLOATS), device=dev)
+    mean = torch.empty((B, 64), device=dev) if critic else None
+    save_c = torch.empty((2, B, R, 64), device=dev) if critic else None
+    L, st = _native.lib(), torch.cuda.current_stream().cuda_stream
+    _native.check(L.lb_ds_train_forward(frag.data_ptr(), x.data_ptr(), B, R, logits.data_ptr(), fused._ptr(mean),
+                                        save_a.data_ptr(), fused._ptr(save_c), setvec.data_ptr(), st))
+    bfrag = fused_train._pack_backward(agent.actor.net, crit, dev)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    dl = torch.randn((B, R), generator=g, device=dev)
+    dm = torch.randn((B, 64), generator=g, device=dev) if critic else None
+    n = _native.LB_DS_SETGRAD_ACTOR + (_native.LB_DS_SETGRAD_CRITIC if critic else 0)
+    out = []
+    for merged in (False, True):
+        wg = torch.empty((2, _native.LB_DS_WGRAD_FLOATS), device=dev)
+        sg = torch.empty(n, device=dev)
+        args = (bfrag.data_ptr(), x.data_ptr(), B, R, save_a.data_ptr(), fused._ptr(save_c), dl.data_ptr(),
+                fused._ptr(dm), wg.data_ptr(), fused_train._workspace(dev).data_ptr(), setvec.data_ptr())
+        if merged:
+            _native.check(L.lb_ds_train_backward_sets(*args, sg.data_ptr(), st))
+        else:
+            _native.check(L.lb_ds_train_backward(*args, st))
+            _native.check(L.lb_ds_set_grads(setvec.data_ptr(), dl.data_ptr(), fused._ptr(dm), B, R, sg.data_ptr(), st))
+        out.append((wg, sg))
+    torch.cuda.synchronize()
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
