@@ -10,8 +10,8 @@
 // config 5 (4096 envs) the step and replay kernels were ~5 us each of mostly launch ramp and
 // tail (profiles/r03_dqn_kernel_stats_setgrads.csv); here they follow the forward inside the
 // same waves.  Same functions, same order per env: bit for bit the three launches
-// (tests/test_gpu_dqn_step.py).  The launch takes P = LB_DQN_P (2) envs per wave iteration
-// (lbk8s.hip: dqn_steps_launch); P = 4 is the other instantiation.
+// (tests/test_gpu_dqn_step.py).  The launch takes P = 2 envs per wave iteration (lbk8s.hip:
+// dqn_steps_launch; one env per wave measured slower: profiles/r06_dqn_p1_ab.jsonl).
 #pragma once
 
 #include "lbk8s_deepsets.h"
