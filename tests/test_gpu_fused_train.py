@@ -82,6 +82,28 @@ def test_train_step_matches_autograd(R, ties):
         _check(p.grad, q.grad, f"grad {name} R={R}", 1e-3, 1e-4)
 
 
+def test_train_step_extra_row_many_sets_per_wave():
+    """R = 65 (the extra-row training forward, the backward's one-row last tile and its pooled
+    term) with 4,500 sets: more sets than the kernels' 2,048 waves, so waves loop over sets and
+    reuse their LDS scratch and pooled-term rows; actor and critic against float64 autograd."""
+    from lbk8s import fused_train
+    agent = _agent(65)
+    B, R = 4500, 65
+    x = _inputs(B, R, seed=77, ties=True)
+    g = torch.Generator().manual_seed(78)
+    wl, wv = torch.randn(B, R, generator=g), torch.randn(B, generator=g)
+    ref = copy.deepcopy(agent).double()
+    xl, vl = ref.actor(x.double()), ref.critic(x.double())
+    ((xl * wl.double()).sum() + (vl * wv.double()).sum()).backward()
+    dev = agent.cuda()
+    logits, value = fused_train.actor_critic(dev, x.cuda())
+    _check(logits, xl, "logits", 1e-4, 4e-6)
+    _check(value, vl, "value", 1e-4, 4e-6)
+    ((logits * wl.cuda()).sum() + (value * wv.cuda()).sum()).backward()
+    for (name, p), (_, q) in zip(dev.named_parameters(), ref.named_parameters()):
+        _check(p.grad, q.grad, f"grad {name}", 1e-3, 1e-4)
+
+
 def test_train_step_actor_only_and_many_sets():
     """The DQN Q network (actor stack only); more sets than resident waves."""
     from lbk8s import fused_train
